@@ -1,0 +1,206 @@
+/*
+ * sdsp.h — C ABI of the MI355X-native streaming filter engine (libsdsp.so).
+ *
+ * Drop-in boundary for juliantos/solid-dsp's hot path.  Every entry point
+ * replaces one method of the reference's Rust API; the reference item it
+ * replaces is cited (paths relative to the reference checkout).  A Rust shim
+ * crate keeps `solid::filter::*` / `solid::dot_product::*` and forwards to
+ * these symbols (INTEGRATION.md shows the bindings).
+ *
+ * Conventions (mirroring the reference):
+ *  - Construction copies taps into the handle (DotProduct::new, alloc_zeroed,
+ *    src/dot_product/mod.rs:57-87) and can fail with the reference's error
+ *    enums (FIRErrorCode src/filter/fir/mod.rs:40-45, IIRErrorCode
+ *    src/filter/iir/mod.rs:41-49, SecondOrderErrorCode src/filter/iir/sos.rs:19-21),
+ *    returned as sdsp_status codes.  Execution cannot fail except for device
+ *    errors (>= SDSP_E_DEVICE); sdsp_last_error() gives the message.
+ *  - Complex samples/taps are interleaved {re, im}, the #[repr(C)] layout of
+ *    num::Complex<T>.
+ *  - A handle is bound to one device and owns: the tap copy, the delay-line
+ *    state (the reference's `Window`, src/window/mod.rs:9-77) resident in HBM,
+ *    one hipStream_t and device staging buffers.  A handle is not thread safe
+ *    (the reference types are !Send); distinct handles may run concurrently.
+ *  - `*_execute_block` takes HOST slices (like `&[In] -> Vec<Out>`) and is
+ *    PCIe-bound; `*_execute_block_device` takes device pointers (HBM resident)
+ *    and a hipStream_t (NULL = the handle's stream) and is asynchronous.
+ *  - No CPU fallback: with no usable gfx950 device every create call returns
+ *    SDSP_E_NO_DEVICE.
+ */
+#ifndef SDSP_H
+#define SDSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDSP_API __attribute__((visibility("default")))
+
+/* (Coef, In) pairs.  Out = Coef * In (num-complex Mul). */
+typedef enum {
+    SDSP_RR32 = 0, /* f32  taps, f32  samples                                  */
+    SDSP_RC32 = 1, /* f32  taps, c32  samples ("crcf")                         */
+    SDSP_CC32 = 2, /* c32  taps, c32  samples ("cccf")                         */
+    SDSP_RR64 = 3, /* f64  taps, f64  samples (the reference Filter path)      */
+    SDSP_RC64 = 4, /* f64  taps, c64  samples (FIRFilter<f64, Complex<f64>>)   */
+    SDSP_CC64 = 5  /* c64  taps, c64  samples                                  */
+} sdsp_dtype;
+
+/* Kernel selection for FIR-type handles. */
+typedef enum {
+    SDSP_ALGO_AUTO = 0,  /* FFT overlap-save for 32-bit complex when it applies, else EXACT */
+    SDSP_ALGO_EXACT = 1, /* direct form in the reference summation order, no FMA contraction:
+                            bit-identical to the reference algorithm at the handle's precision */
+    SDSP_ALGO_FMA = 2,   /* direct form, same order, fused multiply-add                      */
+    SDSP_ALGO_FFT = 3    /* overlap-save fast convolution (N = 4096) in LDS                  */
+} sdsp_algo;
+
+typedef enum {
+    SDSP_OK = 0,
+    /* FIRErrorCode (src/filter/fir/mod.rs:40-45) */
+    SDSP_E_COEFFICIENTS_LENGTH_ZERO = 1,
+    SDSP_E_DECIMATION_LESS_THAN_ONE = 2,
+    SDSP_E_INTERPOLATION_LESS_THAN_ONE = 3,
+    SDSP_E_NOT_ENOUGH_FILTERS = 4,
+    /* IIRErrorCode (src/filter/iir/mod.rs:41-49) */
+    SDSP_E_NUMERATOR_LENGTH_ZERO = 10,
+    SDSP_E_DENOMINATOR_LENGTH_ZERO = 11,
+    SDSP_E_SOS_SIZE_ZERO = 12,
+    SDSP_E_SOS_SIZE_MISMATCH = 13,
+    SDSP_E_SOS_SIZE_NOT_MULTIPLE_OF_3 = 14,
+    SDSP_E_IIR_DECIMATION_LESS_THAN_ONE = 15,
+    SDSP_E_IIR_INTERPOLATION_LESS_THAN_ONE = 16,
+    /* SecondOrderErrorCode (src/filter/iir/sos.rs:19-21) */
+    SDSP_E_SOS_COEFFICIENTS_NOT_IN_RANGE = 20,
+    /* argument errors the reference reports by panicking */
+    SDSP_E_INVALID_ARGUMENT = 90,
+    SDSP_E_UNSUPPORTED = 91,
+    /* device errors */
+    SDSP_E_DEVICE = 100,
+    SDSP_E_NO_DEVICE = 101,
+    SDSP_E_OUT_OF_MEMORY = 102
+} sdsp_status;
+
+SDSP_API const char* sdsp_last_error(void);
+SDSP_API const char* sdsp_version(void);
+/* number of visible gfx950 devices (0 when none) */
+SDSP_API int sdsp_device_count(void);
+/* bytes of one sample / one tap of a dtype */
+SDSP_API size_t sdsp_sample_size(int dtype);
+SDSP_API size_t sdsp_coef_size(int dtype);
+
+/* ------------------------------------------------------------------------
+ * FIR and decimating FIR  (FIRFilter src/filter/fir/mod.rs:58-304,
+ *                          DecimatingFIRFilter src/filter/fir/decim.rs:5-281)
+ * A FIR handle is a DecimatingFIRFilter with decimation 1.  `channels`
+ * independent delay lines share the taps; device/host buffers are
+ * channel-major: sample i of channel c at [c * n + i].
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_fir sdsp_fir;
+
+/* FIRFilter::new(&[Coef], scale)                    src/filter/fir/mod.rs:79-88 */
+SDSP_API int sdsp_fir_create(sdsp_fir** out, int dtype, const void* taps, size_t len,
+                             const void* scale, int device);
+/* DecimatingFIRFilter::new(&[Coef], scale, M)       src/filter/fir/decim.rs:27-42 */
+SDSP_API int sdsp_decim_create(sdsp_fir** out, int dtype, const void* taps, size_t len,
+                               const void* scale, size_t decimation, int device);
+/* channel count (default 1); resets the delay lines */
+SDSP_API int sdsp_fir_set_channels(sdsp_fir* h, size_t channels);
+SDSP_API int sdsp_fir_set_algo(sdsp_fir* h, int algo);
+SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
+SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */
+/* Clone (derive(Clone), fir/mod.rs:58): same taps and a snapshot of the delay line */
+SDSP_API int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out);
+/* set_scale / get_scale                              fir/mod.rs:103-124, decim.rs:57-78 */
+SDSP_API int sdsp_fir_set_scale(sdsp_fir* h, const void* scale);
+SDSP_API int sdsp_fir_get_scale(const sdsp_fir* h, void* scale);
+/* len (fir/mod.rs:139-142), get_decimation (decim.rs:92-95) */
+SDSP_API size_t sdsp_fir_len(const sdsp_fir* h);
+SDSP_API size_t sdsp_fir_decimation(const sdsp_fir* h);
+/* coefficients(): the stored (REVERSED) taps, as DotProduct::coefficents (fir/mod.rs:173-176) */
+SDSP_API int sdsp_fir_coefficients(const sdsp_fir* h, void* out_len_taps);
+/* number of outputs a block of n inputs produces from the current phase */
+SDSP_API size_t sdsp_fir_output_count(const sdsp_fir* h, size_t n);
+/* Filter::execute(sample) -> Vec<Out> (0 or 1 outputs)  fir/mod.rs:209-212, decim.rs:221-228
+ * (single channel handles only) *n_out = 0/1 */
+SDSP_API int sdsp_fir_execute(sdsp_fir* h, const void* sample, void* out, size_t* n_out);
+/* Filter::execute_block(&[In]) -> Vec<Out>          fir/mod.rs:235-241, decim.rs:250-256
+ * in: channels*n host samples; out: channels*output_count(n) host samples */
+SDSP_API int sdsp_fir_execute_block(sdsp_fir* h, const void* in, size_t n, void* out, size_t* n_out);
+/* device-resident variant (asynchronous on `stream`; NULL = handle stream) */
+SDSP_API int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void* d_out,
+                                           size_t* n_out, void* stream);
+/* DecimatingFIRFilter::push / write (advance phase, no output)  decim.rs:115-118, 136-139 */
+SDSP_API int sdsp_decim_push(sdsp_fir* h, const void* sample);
+SDSP_API int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n);
+/* reset: zero the delay lines and the phase (Window::reset, src/window/mod.rs:54-56) */
+SDSP_API int sdsp_fir_reset(sdsp_fir* h);
+/* delay-line state: the last len-1 inputs per channel, oldest first (+ the phase) */
+SDSP_API size_t sdsp_fir_state_len(const sdsp_fir* h);
+SDSP_API int sdsp_fir_get_state(const sdsp_fir* h, void* hist, size_t* phase);
+SDSP_API int sdsp_fir_set_state(sdsp_fir* h, const void* hist, size_t phase);
+/* Filter::frequency_response / group_delay (host f64)   fir/mod.rs:263-303 */
+SDSP_API int sdsp_fir_frequency_response(const sdsp_fir* h, double f, double* re_im);
+SDSP_API int sdsp_fir_group_delay(const sdsp_fir* h, double f, double* delay);
+SDSP_API int sdsp_fir_synchronize(sdsp_fir* h);
+
+/* ------------------------------------------------------------------------
+ * Polyphase filterbank and interpolating FIR
+ *  (PolyPhaseFilterBank src/filter/fir/pfb.rs:3-91,
+ *   InterpolatingFIRFilter src/filter/fir/interp.rs:6-138)
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_pfb sdsp_pfb;
+
+/* PolyPhaseFilterBank::new(&[Coef], filters, scale)  pfb.rs:24-49 */
+SDSP_API int sdsp_pfb_create(sdsp_pfb** out, int dtype, const void* taps, size_t len, size_t filters,
+                             const void* scale, int device);
+/* InterpolatingFIRFilter::new(&[Coef], M)            interp.rs:27-54 */
+SDSP_API int sdsp_interp_create(sdsp_pfb** out, int dtype, const void* taps, size_t len,
+                                size_t interpolation, int device);
+SDSP_API void sdsp_pfb_destroy(sdsp_pfb* h);
+SDSP_API int sdsp_pfb_clone(const sdsp_pfb* h, sdsp_pfb** out);
+SDSP_API size_t sdsp_pfb_len(const sdsp_pfb* h);          /* number of filters M */
+SDSP_API size_t sdsp_pfb_subfilter_len(const sdsp_pfb* h); /* K */
+SDSP_API int sdsp_pfb_set_scale(sdsp_pfb* h, const void* scale);
+SDSP_API int sdsp_pfb_get_scale(const sdsp_pfb* h, void* scale);
+/* coefficents(): M x K branch coefficients (stored order) */
+SDSP_API int sdsp_pfb_coefficients(const sdsp_pfb* h, void* out_mk);
+/* push(sample)  pfb.rs:81-83 */
+SDSP_API int sdsp_pfb_push(sdsp_pfb* h, const void* sample);
+/* execute(index) on the current window  pfb.rs:85-90 */
+SDSP_API int sdsp_pfb_execute(sdsp_pfb* h, size_t index, void* out);
+/* reset  pfb.rs:77-79 */
+SDSP_API int sdsp_pfb_reset(sdsp_pfb* h);
+/* for each input: push, then all M branch outputs -> out[n*M]
+ * (InterpolatingFIRFilter::execute_block  interp.rs:102-111) */
+SDSP_API int sdsp_pfb_execute_block(sdsp_pfb* h, const void* in, size_t n, void* out);
+SDSP_API int sdsp_pfb_execute_block_device(sdsp_pfb* h, const void* d_in, size_t n, void* d_out, void* stream);
+SDSP_API int sdsp_pfb_frequency_response(const sdsp_pfb* h, double f, double* re_im);
+SDSP_API int sdsp_pfb_group_delay(const sdsp_pfb* h, double f, double* delay);
+SDSP_API int sdsp_pfb_synchronize(sdsp_pfb* h);
+
+/* ------------------------------------------------------------------------
+ * Device utilities
+ * ------------------------------------------------------------------------ */
+/* Synthetic stream (build-defined): `count` f32 scalars
+ * x(i) = ((mix64(seed ^ channel*G + (start+i+1)*G) >> 40) * 2^-24) * 2 - 1 */
+SDSP_API int sdsp_synth_f32_device(void* d_out, uint64_t seed, uint64_t channel, uint64_t start,
+                                   size_t count, void* stream);
+/* Host-side reference FIR tap design (src/filter/firdes/mod.rs:278-305) */
+SDSP_API int sdsp_firdes_kaiser(size_t n, double fc, double as, double mu, double* h);
+SDSP_API int sdsp_firdes_notch(size_t m, double f0, double as, double* h);
+SDSP_API double sdsp_kaiser_beta(double as);
+/* PLL loop filters (src/filter/iirdes/pll/mod.rs:24-99) */
+SDSP_API int sdsp_active_lag(double bw, double zeta, double k, double* num3, double* den3);
+SDSP_API int sdsp_active_proportional_integral(double bw, double zeta, double k, double* num3, double* den3);
+/* group delay helpers (src/group_delay/mod.rs:51-129) */
+SDSP_API int sdsp_fir_group_delay_taps(const double* h, size_t n, double f, double* out);
+SDSP_API int sdsp_iir_group_delay_taps(const double* b, size_t nb, const double* a, size_t na, double f,
+                                       double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDSP_H */

@@ -1,0 +1,19 @@
+"""solid_dsp_amd — MI355X-native streaming FIR / polyphase / IIR engine.
+
+Drop-in for juliantos/solid-dsp's ``filter::*`` / ``dot_product::*`` hot
+path.  The compute runs in hand-written gfx950 HIP kernels inside
+``_build/libsdsp.so`` (C ABI: ``include/sdsp.h``); this package is a thin
+host mirror of the reference's Rust API (module paths, constructor
+arguments, error codes).  There is no CPU execution path.
+"""
+from ._lib import (SdspError, lib, LIB_PATH, RR32, RC32, CC32, RR64, RC64, CC64,  # noqa: F401
+                   ALGO_AUTO, ALGO_EXACT, ALGO_FMA, ALGO_FFT)
+from . import filter, group_delay  # noqa: F401
+from .filter import (Filter, FIRFilter, DecimatingFIRFilter, PolyPhaseFilterBank,  # noqa: F401
+                     InterpolatingFIRFilter)
+
+__version__ = "0.1.0"
+
+
+def device_count() -> int:
+    return int(lib().sdsp_device_count())

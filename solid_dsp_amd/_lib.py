@@ -1,0 +1,224 @@
+"""Loader for libsdsp.so, the gfx950 C-ABI library (include/sdsp.h).
+
+The library is built in-tree (``solid_dsp_amd/_build/libsdsp.so``) by
+``__graft_entry__.build()`` / ``make -C solid_dsp_amd/csrc``.  There is no
+pure-Python or CPU fallback: if the library is missing, or no gfx950 device is
+visible when a filter is constructed, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "_build", "libsdsp.so")
+
+# sdsp_dtype (Coef, In)
+RR32, RC32, CC32, RR64, RC64, CC64 = range(6)
+ALGO_AUTO, ALGO_EXACT, ALGO_FMA, ALGO_FFT = range(4)
+
+_PAIRS = {
+    (np.dtype(np.float32), np.dtype(np.float32)): RR32,
+    (np.dtype(np.float32), np.dtype(np.complex64)): RC32,
+    (np.dtype(np.complex64), np.dtype(np.complex64)): CC32,
+    (np.dtype(np.float64), np.dtype(np.float64)): RR64,
+    (np.dtype(np.float64), np.dtype(np.complex128)): RC64,
+    (np.dtype(np.complex128), np.dtype(np.complex128)): CC64,
+}
+COEF_DTYPE = {v: k[0] for k, v in _PAIRS.items()}
+SAMPLE_DTYPE = {v: k[1] for k, v in _PAIRS.items()}
+
+STATUS = {
+    0: "Ok",
+    1: "CoefficientsLengthZero", 2: "DecimationLessThanOne", 3: "InterpolationLessThanOne",
+    4: "NotEnoughFilters",
+    10: "NumeratorLengthZero", 11: "DenominatorLengthZero", 12: "SecondOrderSectionSizeZero",
+    13: "SecondOrderSectionSizeMismatch", 14: "SecondOrderSectionSizeNotMultpleOf3",
+    15: "DecimationLessThanOne", 16: "InterpolationLessThanOne",
+    20: "CoefficientsNotInRange",
+    90: "InvalidArgument", 91: "Unsupported",
+    100: "DeviceError", 101: "NoDevice", 102: "OutOfMemory",
+}
+
+
+class SdspError(RuntimeError):
+    """A non-zero sdsp_status.  ``code`` mirrors the reference error enums."""
+
+    def __init__(self, code: int, msg: str = ""):
+        self.code = code
+        self.name = STATUS.get(code, f"status {code}")
+        super().__init__(f"{self.name} ({code}){': ' + msg if msg else ''}")
+
+
+def dtype_code(coef_dtype, sample_dtype) -> int:
+    key = (np.dtype(coef_dtype), np.dtype(sample_dtype))
+    if key not in _PAIRS:
+        raise TypeError(f"unsupported (Coef, In) pair {key}")
+    return _PAIRS[key]
+
+
+_lib = None
+
+
+def _declare(L):
+    vp, sz, i, d, dp, szp = C.c_void_p, C.c_size_t, C.c_int, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_size_t)
+    vpp = C.POINTER(C.c_void_p)
+    sig = {
+        "sdsp_last_error": (C.c_char_p, []),
+        "sdsp_version": (C.c_char_p, []),
+        "sdsp_device_count": (i, []),
+        "sdsp_sample_size": (sz, [i]),
+        "sdsp_coef_size": (sz, [i]),
+        "sdsp_fir_create": (i, [vpp, i, vp, sz, vp, i]),
+        "sdsp_decim_create": (i, [vpp, i, vp, sz, vp, sz, i]),
+        "sdsp_fir_set_channels": (i, [vp, sz]),
+        "sdsp_fir_set_algo": (i, [vp, i]),
+        "sdsp_fir_get_algo": (i, [vp]),
+        "sdsp_fir_destroy": (None, [vp]),
+        "sdsp_fir_clone": (i, [vp, vpp]),
+        "sdsp_fir_set_scale": (i, [vp, vp]),
+        "sdsp_fir_get_scale": (i, [vp, vp]),
+        "sdsp_fir_len": (sz, [vp]),
+        "sdsp_fir_decimation": (sz, [vp]),
+        "sdsp_fir_coefficients": (i, [vp, vp]),
+        "sdsp_fir_output_count": (sz, [vp, sz]),
+        "sdsp_fir_execute": (i, [vp, vp, vp, szp]),
+        "sdsp_fir_execute_block": (i, [vp, vp, sz, vp, szp]),
+        "sdsp_fir_execute_block_device": (i, [vp, vp, sz, vp, szp, vp]),
+        "sdsp_decim_push": (i, [vp, vp]),
+        "sdsp_decim_write": (i, [vp, vp, sz]),
+        "sdsp_fir_reset": (i, [vp]),
+        "sdsp_fir_state_len": (sz, [vp]),
+        "sdsp_fir_get_state": (i, [vp, vp, szp]),
+        "sdsp_fir_set_state": (i, [vp, vp, sz]),
+        "sdsp_fir_frequency_response": (i, [vp, d, dp]),
+        "sdsp_fir_group_delay": (i, [vp, d, dp]),
+        "sdsp_fir_synchronize": (i, [vp]),
+        "sdsp_pfb_create": (i, [vpp, i, vp, sz, sz, vp, i]),
+        "sdsp_interp_create": (i, [vpp, i, vp, sz, sz, i]),
+        "sdsp_pfb_destroy": (None, [vp]),
+        "sdsp_pfb_clone": (i, [vp, vpp]),
+        "sdsp_pfb_len": (sz, [vp]),
+        "sdsp_pfb_subfilter_len": (sz, [vp]),
+        "sdsp_pfb_set_scale": (i, [vp, vp]),
+        "sdsp_pfb_get_scale": (i, [vp, vp]),
+        "sdsp_pfb_coefficients": (i, [vp, vp]),
+        "sdsp_pfb_push": (i, [vp, vp]),
+        "sdsp_pfb_execute": (i, [vp, sz, vp]),
+        "sdsp_pfb_reset": (i, [vp]),
+        "sdsp_pfb_execute_block": (i, [vp, vp, sz, vp]),
+        "sdsp_pfb_execute_block_device": (i, [vp, vp, sz, vp, vp]),
+        "sdsp_pfb_frequency_response": (i, [vp, d, dp]),
+        "sdsp_pfb_group_delay": (i, [vp, d, dp]),
+        "sdsp_pfb_synchronize": (i, [vp]),
+        "sdsp_synth_f32_device": (i, [vp, C.c_uint64, C.c_uint64, C.c_uint64, sz, vp]),
+        "sdsp_firdes_kaiser": (i, [sz, d, d, d, dp]),
+        "sdsp_firdes_notch": (i, [sz, d, d, dp]),
+        "sdsp_kaiser_beta": (d, [d]),
+        "sdsp_active_lag": (i, [d, d, d, dp, dp]),
+        "sdsp_active_proportional_integral": (i, [d, d, d, dp, dp]),
+        "sdsp_fir_group_delay_taps": (i, [dp, sz, d, dp]),
+        "sdsp_iir_group_delay_taps": (i, [dp, sz, dp, sz, d, dp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)  # AttributeError = the .so does not export what include/sdsp.h declares
+        f.restype = res
+        f.argtypes = args
+    # optional families (declared when the library exports them)
+    for name, (res, args) in _optional_sigs().items():
+        if hasattr(L, name):
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+
+
+def _optional_sigs():
+    vp, sz, i, d, dp, szp = C.c_void_p, C.c_size_t, C.c_int, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_size_t)
+    vpp = C.POINTER(C.c_void_p)
+    return {
+        "sdsp_iir_create": (i, [vpp, i, vp, sz, vp, sz, i, i]),
+        "sdsp_iir_decim_create": (i, [vpp, i, vp, sz, vp, sz, i, sz, i]),
+        "sdsp_iir_interp_create": (i, [vpp, i, vp, sz, vp, sz, i, sz, i]),
+        "sdsp_iir_destroy": (None, [vp]),
+        "sdsp_iir_clone": (i, [vp, vpp]),
+        "sdsp_iir_set_channels": (i, [vp, sz]),
+        "sdsp_iir_set_algo": (i, [vp, i]),
+        "sdsp_iir_output_count": (sz, [vp, sz]),
+        "sdsp_iir_execute_block": (i, [vp, vp, sz, vp, szp]),
+        "sdsp_iir_execute_block_device": (i, [vp, vp, sz, vp, szp, vp]),
+        "sdsp_iir_reset": (i, [vp]),
+        "sdsp_iir_state_len": (sz, [vp]),
+        "sdsp_iir_get_state": (i, [vp, vp, szp]),
+        "sdsp_iir_set_state": (i, [vp, vp, sz]),
+        "sdsp_iir_frequency_response": (i, [vp, d, dp]),
+        "sdsp_iir_group_delay": (i, [vp, d, dp]),
+        "sdsp_iir_coefficients": (i, [vp, dp, dp]),
+        "sdsp_iir_num_coefs": (sz, [vp, i]),
+        "sdsp_iir_synchronize": (i, [vp]),
+        "sdsp_sos_create": (i, [vpp, C.POINTER(C.c_double), sz, C.POINTER(C.c_double), sz, i]),
+        "sdsp_chan_create": (i, [vpp, vp, sz, sz, i]),
+        "sdsp_chan_destroy": (None, [vp]),
+        "sdsp_chan_set_streams": (i, [vp, sz]),
+        "sdsp_chan_execute_block_device": (i, [vp, vp, sz, vp, szp, vp]),
+        "sdsp_chan_execute_block": (i, [vp, vp, sz, vp, szp]),
+        "sdsp_chan_reset": (i, [vp]),
+        "sdsp_chan_synchronize": (i, [vp]),
+        "sdsp_fft_create": (i, [vpp, sz, i, i]),
+        "sdsp_fft_destroy": (None, [vp]),
+        "sdsp_fft_execute": (i, [vp, vp, vp, sz]),
+        "sdsp_fft_execute_device": (i, [vp, vp, vp, sz, vp]),
+        "sdsp_dot_execute_batched_device": (i, [i, vp, sz, i, vp, sz, sz, vp, vp]),
+        "sdsp_dot_execute": (i, [i, vp, sz, i, vp, sz, vp]),
+    }
+
+
+def lib():
+    """The loaded libsdsp.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        # One HIP runtime per process: torch wheels bundle their own
+        # libamdhip64.so (soname libamdhip64.so.7).  Importing torch first makes
+        # libsdsp.so bind to that already-loaded runtime, so torch tensors,
+        # torch streams and our kernels share one device context.
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover - torch is plumbing, not required
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C solid_dsp_amd/csrc` (there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc != 0:
+        raise SdspError(rc, lib().sdsp_last_error().decode(errors="replace"))
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def device_ptr(t) -> int:
+    """Raw device pointer of a torch tensor / int (torch is plumbing only)."""
+    if isinstance(t, int):
+        return t
+    return int(t.data_ptr())
+
+
+def stream_handle(stream) -> int | None:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)

@@ -1,0 +1,241 @@
+// Overlap-save fast-convolution FIR for 32-bit complex streams (gfx950).
+//
+// Same filter as FIRFilter::execute (src/filter/fir/mod.rs:209-212):
+//     y[n] = scale * sum_{i<L} h[L-1-i] x[n-i]
+// computed per 4096-sample segment as a circular convolution with the
+// zero-padded impulse response g[i] = scale*h[L-1-i] (spectrum precomputed in
+// f64 on the host).  Segment s reads x[s*V - H, s*V - H + 4096) and writes the
+// V = 4096 - H outputs that do not wrap (H = 256*h2 >= L-1).
+//
+// Data flow (one 256-thread workgroup per segment, 16 points per lane, all
+// three radix-16 passes of the forward DIF FFT, the spectral multiply and
+// the three passes of the inverse in registers; the segment visits LDS only
+// for the four transposes between passes):
+//     n = 256 n2 + 16 n1 + n0,  k = k0 + 16 k1 + 256 k2
+//   load   lane t=(n1,n0)   holds x over n2     (coalesced: stride 256 samples)
+//   P1     DFT16 n2->k0, * W4096^(t k0)        -> LDS A[k0][t]
+//   P2     lane (k0,n0)     DFT16 n1->k1, * W256^(n0 k1) -> LDS B[k0,k1][n0]
+//   P3     lane (k0,k1)     DFT16 n0->k2, * H[k0+16k1+256k2]/N,
+//                           IDFT16 k2->n0, * W256^-(k1 n0) -> LDS B
+//   P4     lane (k0,n0)     IDFT16 k1->n1                    -> LDS A
+//   P5     lane t=(n1,n0)   * W4096^-(t k0), IDFT16 k0->n2, store n2 >= h2
+// The DIF output order is exactly the order the inverse DIT consumes, so no
+// bit-reversal pass exists.  Twiddle rows and the spectrum slice each lane
+// needs are constant across segments and live in registers; the workgroup is
+// persistent over a contiguous run of segments so each segment's halo is an
+// L2 hit on the previous segment's tail.
+#include "sdsp_device.hpp"
+#include "sdsp_kernels.hpp"
+
+namespace sdsp {
+
+namespace {
+
+struct cf { float re, im; };
+
+__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.re + b.re, a.im + b.im}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return {a.re - b.re, a.im - b.im}; }
+__device__ __forceinline__ cf cmul(cf a, cf b) {
+    return {__builtin_fmaf(a.re, b.re, -(a.im * b.im)), __builtin_fmaf(a.re, b.im, a.im * b.re)};
+}
+__device__ __forceinline__ cf cmulc(cf a, cf b) {  // a * conj(b)
+    return {__builtin_fmaf(a.re, b.re, a.im * b.im), __builtin_fmaf(a.im, b.re, -(a.re * b.im))};
+}
+// multiply by -j (forward) / +j (inverse)
+template <bool INV> __device__ __forceinline__ cf rotj(cf a) {
+    if constexpr (INV) return {-a.im, a.re};
+    else return {a.im, -a.re};
+}
+
+template <bool INV> __device__ __forceinline__ void dft4(cf& x0, cf& x1, cf& x2, cf& x3) {
+    cf a = cadd(x0, x2), b = csub(x0, x2), c = cadd(x1, x3), d = rotj<INV>(csub(x1, x3));
+    x0 = cadd(a, c);
+    x2 = csub(a, c);
+    x1 = cadd(b, d);
+    x3 = csub(b, d);
+}
+
+constexpr float kC1 = 0.92387953251128674f;  // cos(pi/8)
+constexpr float kS1 = 0.38268343236508978f;  // sin(pi/8)
+constexpr float kR2 = 0.70710678118654752f;  // sqrt(1/2)
+
+// v *= W16^m (forward: e^{-j 2 pi m/16}; inverse: conjugate)
+template <bool INV, int m> __device__ __forceinline__ cf tw16(cf v) {
+    constexpr float s = INV ? -1.0f : 1.0f;
+    if constexpr (m == 0) return v;
+    else if constexpr (m == 1) return cmul(v, cf{kC1, -s * kS1});
+    else if constexpr (m == 2) return cf{kR2 * (v.re + s * v.im), kR2 * (v.im - s * v.re)};
+    else if constexpr (m == 3) return cmul(v, cf{kS1, -s * kC1});
+    else if constexpr (m == 4) return rotj<INV>(v);
+    else if constexpr (m == 6) return cf{kR2 * (-v.re + s * v.im), kR2 * (-v.im - s * v.re)};
+    else if constexpr (m == 9) return cmul(v, cf{-kC1, s * kS1});
+    else return v;
+}
+
+// in-place 16-point DFT, natural order in and out
+template <bool INV> __device__ __forceinline__ void dft16(cf (&v)[16]) {
+    // n = 4 na + nb ; k = ka + 4 kb
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) dft4<INV>(v[nb], v[4 + nb], v[8 + nb], v[12 + nb]);
+    // v[4 ka + nb] now holds stage-1 output (nb, ka); twiddle W16^(nb ka)
+    v[5] = tw16<INV, 1>(v[5]);
+    v[6] = tw16<INV, 2>(v[6]);
+    v[7] = tw16<INV, 3>(v[7]);
+    v[9] = tw16<INV, 2>(v[9]);
+    v[10] = tw16<INV, 4>(v[10]);
+    v[11] = tw16<INV, 6>(v[11]);
+    v[13] = tw16<INV, 3>(v[13]);
+    v[14] = tw16<INV, 6>(v[14]);
+    v[15] = tw16<INV, 9>(v[15]);
+#pragma unroll
+    for (int ka = 0; ka < 4; ++ka) dft4<INV>(v[4 * ka + 0], v[4 * ka + 1], v[4 * ka + 2], v[4 * ka + 3]);
+    // v[4 ka + kb] = X[ka + 4 kb]  -> transpose to natural order
+    cf t[16];
+#pragma unroll
+    for (int ka = 0; ka < 4; ++ka)
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) t[ka + 4 * kb] = v[4 * ka + kb];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = t[i];
+}
+
+constexpr int kRowA = 272;  // A image: 16 rows of 256 (+16 pad) samples
+constexpr int kRegion = 16 * kRowA;  // samples per LDS region
+
+// B image: 256 rows x 16 samples, pairs XOR-swizzled by (row>>1)&7
+__device__ __forceinline__ int bidx(int r, int c) { return r * 16 + ((((c >> 1) ^ (r >> 1)) & 7) << 1) + (c & 1); }
+
+template <bool CHECK>
+__device__ __forceinline__ void load_seg(cf (&v)[16], const cf* __restrict__ x, const cf* __restrict__ hist,
+                                         long long base, int t, long long n, int Lm1) {
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) {
+        const long long j = base + 256 * n2 + t;
+        if constexpr (!CHECK) {
+            v[n2] = x[j];
+        } else {
+            cf s = {0.0f, 0.0f};
+            if (j >= 0) {
+                if (j < n) s = x[j];
+            } else if (Lm1 + j >= 0) {
+                s = hist[Lm1 + j];
+            }
+            v[n2] = s;
+        }
+    }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256, 2)
+fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const cf* __restrict__ Hs,
+                   const cf* __restrict__ tw1, const cf* __restrict__ tw2, cf* __restrict__ y, long long n,
+                   int Lm1, int h2, long long nseg, long long segs_per_block) {
+    __shared__ __attribute__((aligned(16))) cf lds[2 * kRegion];
+    cf* const rA = lds;
+    cf* const rB = lds + kRegion;
+    const int ch = blockIdx.y;
+    x += (long long)ch * n;
+    y += (long long)ch * n;
+    hist += (long long)ch * Lm1;
+
+    const int t = threadIdx.x;
+    const int hi4 = t >> 4, lo4 = t & 15;
+    cf w1[16], w2[16], Hr[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        w1[k] = tw1[t * 16 + k];
+        w2[k] = tw2[lo4 * 16 + k];
+        Hr[k] = Hs[t * 16 + k];
+    }
+    const int V = 4096 - 256 * h2;
+    long long s0 = (long long)blockIdx.x * segs_per_block;
+    long long s1 = s0 + segs_per_block;
+    if (s1 > nseg) s1 = nseg;
+
+    for (long long seg = s0; seg < s1; ++seg) {
+        cf v[16];
+        const long long base = seg * V - 256 * h2;
+        if (base >= 0 && base + 4096 <= n) load_seg<false>(v, x, hist, base, t, n, Lm1);
+        else load_seg<true>(v, x, hist, base, t, n, Lm1);
+
+        // P1: DFT over n2 -> k0, twiddle, A[k0][t]
+        dft16<false>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rA[k * kRowA + t] = cmul(v[k], w1[k]);
+        __syncthreads();
+        // P2: lane (k0=hi4, n0=lo4) reads n1
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = rA[hi4 * kRowA + 16 * k + lo4];
+        dft16<false>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rB[bidx(16 * hi4 + k, lo4)] = cmul(v[k], w2[k]);
+        __syncthreads();
+        // P3: lane (k0=hi4, k1=lo4) reads its row over n0
+        {
+            const float4* row = reinterpret_cast<const float4*>(rB + t * 16);
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const float4 q = row[(p ^ (t >> 1)) & 7];
+                v[2 * p] = {q.x, q.y};
+                v[2 * p + 1] = {q.z, q.w};
+            }
+        }
+        dft16<false>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = cmul(v[k], Hr[k]);
+        dft16<true>(v);
+        // back to A region (its readers all passed the barrier above)
+        {
+            float4* row = reinterpret_cast<float4*>(rA + t * 16);
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const cf a = cmulc(v[2 * p], w2[2 * p]);
+                const cf b = cmulc(v[2 * p + 1], w2[2 * p + 1]);
+                row[(p ^ (t >> 1)) & 7] = make_float4(a.re, a.im, b.re, b.im);
+            }
+        }
+        __syncthreads();
+        // P4: lane (k0=hi4, n0=lo4) reads k1
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = rA[bidx(16 * hi4 + k, lo4)];
+        dft16<true>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rB[hi4 * kRowA + 16 * k + lo4] = v[k];
+        __syncthreads();
+        // P5: lane t=(n1,n0) reads k0
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = cmulc(rB[k * kRowA + t], w1[k]);
+        dft16<true>(v);
+        const long long ob = seg * V - 256 * h2 + t;
+        if (ob + 256 * 16 <= n) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k >= h2) y[ob + 256 * k] = v[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k >= h2 && ob + 256 * k < n) y[ob + 256 * k] = v[k];
+        }
+        // next segment's P1 writes region A: every lane has finished reading
+        // region A (P4) before the barrier that precedes P5.
+    }
+}
+
+hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
+                          size_t channels, int num_cus, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int h2 = p.halo_rows;
+    const long long V = 4096 - 256 * h2;
+    const long long nseg = ((long long)n + V - 1) / V;
+    long long blocks = (long long)num_cus * 2;
+    long long per = (nseg + blocks - 1) / blocks;
+    if (per < 1) per = 1;
+    blocks = (nseg + per - 1) / per;
+    dim3 grid((unsigned)blocks, (unsigned)channels);
+    hipLaunchKernelGGL(fir_ols4096_kernel, grid, dim3(256), 0, s, (const cf*)x, (const cf*)hist, (const cf*)p.d_H,
+                       (const cf*)p.d_tw1, (const cf*)p.d_tw2, (cf*)y, (long long)n, L - 1, h2, nseg, per);
+    return hipGetLastError();
+}
+
+}  // namespace sdsp

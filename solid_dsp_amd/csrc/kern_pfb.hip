@@ -1,0 +1,100 @@
+// Polyphase filterbank / interpolating FIR kernel (gfx950).
+//
+// PolyPhaseFilterBank (src/filter/fir/pfb.rs:24-90): branch p holds
+// cb[p][i] = h[p + (K-1-i) M] (stored FORWARD after the in-place reversal at
+// pfb.rs:33-40) and execute(p) = sum_{i<K} cb[p][i] * w[i] over the shared
+// newest-first Window(K) — no scale.  InterpolatingFIRFilter::execute_block
+// (src/filter/fir/interp.rs:102-111) pushes each input and emits all M
+// branches, so
+//     out[j*M + p] = sum_{i<K} cb[p][i] * x[j-i]
+// Each lane owns one output; lanes of a wave cover consecutive (j, p) so the
+// stores are contiguous, the sample x[j-i] is a broadcast within the wave and
+// the M*K coefficients stay L1/L2 resident.  Summation order is the
+// reference's (EXACT) or fused.
+#include "sdsp_device.hpp"
+#include "sdsp_kernels.hpp"
+
+namespace sdsp {
+
+template <typename I>
+__device__ inline I pfb_ext(const I* __restrict__ x, const I* __restrict__ hist, long long j, int H) {
+    if (j >= 0) return x[j];
+    const long long h = (long long)H + j;
+    return h >= 0 ? hist[h] : zero_v<I>();
+}
+
+template <typename C, typename I, bool EXACT>
+__global__ void __launch_bounds__(256)
+pfb_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* __restrict__ cb, I* __restrict__ y,
+           long long n, int K, int M, int H) {
+    const int ch = blockIdx.y;
+    x += (long long)ch * n;
+    hist += (long long)ch * H;
+    const long long total = n * M;
+    y += (long long)ch * total;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+        const long long j = o / M;
+        const int p = (int)(o - j * M);
+        const C* c = cb + (long long)p * K;
+        I acc = zero_v<I>();
+        for (int i = 0; i < K; ++i) acc = mac<EXACT>(acc, c[i], pfb_ext(x, hist, j - i, H));
+        y[o] = acc;
+    }
+}
+
+template <typename C, typename I>
+hipError_t launch_pfb_t(const PfbArgs& a, hipStream_t s) {
+    const long long total = (long long)a.n * a.M;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    dim3 grid((unsigned)blocks, (unsigned)a.channels);
+    if (a.exact)
+        hipLaunchKernelGGL((pfb_kernel<C, I, true>), grid, dim3(256), 0, s, (const I*)a.x, (const I*)a.hist,
+                           (const C*)a.cb, (I*)a.y, (long long)a.n, a.K, a.M, a.H);
+    else
+        hipLaunchKernelGGL((pfb_kernel<C, I, false>), grid, dim3(256), 0, s, (const I*)a.x, (const I*)a.hist,
+                           (const C*)a.cb, (I*)a.y, (long long)a.n, a.K, a.M, a.H);
+    return hipGetLastError();
+}
+
+hipError_t launch_pfb(int dtype, const PfbArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    switch (dtype) {
+        case 0: return launch_pfb_t<float, float>(a, s);
+        case 1: return launch_pfb_t<float, c32>(a, s);
+        case 2: return launch_pfb_t<c32, c32>(a, s);
+        case 3: return launch_pfb_t<double, double>(a, s);
+        case 4: return launch_pfb_t<double, c64>(a, s);
+        case 5: return launch_pfb_t<c64, c64>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+// ---- synthetic stream (build-defined generator) ---------------
+__device__ inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ void synth_kernel(float* __restrict__ out, uint64_t key, uint64_t start, long long count) {
+    const uint64_t g = 0x9E3779B97F4A7C15ULL;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < count; j += stride) {
+        const uint64_t v = mix64(key + (start + (uint64_t)j + 1) * g);
+        out[j] = (float)(v >> 40) * (1.0f / 16777216.0f) * 2.0f - 1.0f;
+    }
+}
+
+hipError_t launch_synth_f32(float* out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,
+                            hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const uint64_t key = seed ^ (channel * 0x9E3779B97F4A7C15ULL);
+    long long blocks = ((long long)count + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, s, out, key, start, (long long)count);
+    return hipGetLastError();
+}
+
+}  // namespace sdsp

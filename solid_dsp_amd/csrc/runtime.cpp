@@ -1,0 +1,775 @@
+// C-ABI runtime of libsdsp.so: handles, HBM-resident delay lines, streams,
+// kernel selection.  Every exported function cites the reference method it
+// replaces in include/sdsp.h.
+//
+// There is deliberately no CPU execution path: if no gfx950 device is usable
+// the create calls fail with SDSP_E_NO_DEVICE and nothing runs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sdsp.h"
+#include "sdsp_host.hpp"
+#include "sdsp_kernels.hpp"
+
+namespace sdsp {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int device_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return SDSP_OK;
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? SDSP_E_OUT_OF_MEMORY : SDSP_E_DEVICE;
+}
+#define SDSP_TRY(expr, what)                              \
+    do {                                                  \
+        hipError_t _e = (expr);                           \
+        if (_e != hipSuccess) return device_status(_e, what); \
+    } while (0)
+
+struct DeviceInfo {
+    bool ok = false;
+    int cus = 256;
+};
+
+static int check_device(int device, DeviceInfo* info) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+        set_error("no HIP device visible (libsdsp has no CPU execution path)");
+        return SDSP_E_NO_DEVICE;
+    }
+    if (device < 0 || device >= count) {
+        set_error("device index out of range");
+        return SDSP_E_NO_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        set_error("hipGetDeviceProperties failed");
+        return SDSP_E_NO_DEVICE;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("libsdsp is built for gfx950; device is ") + prop.gcnArchName);
+        return SDSP_E_NO_DEVICE;
+    }
+    info->ok = true;
+    info->cus = prop.multiProcessorCount;
+    return SDSP_OK;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int d) {
+        (void)hipGetDevice(&prev);
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+static hipStream_t pick(void* user, hipStream_t own) { return user ? (hipStream_t)user : own; }
+
+}  // namespace sdsp
+
+using namespace sdsp;
+
+// ===========================================================================
+// FIR / decimating FIR
+// ===========================================================================
+struct sdsp_fir {
+    int dtype = 0, device = 0, cus = 256;
+    size_t L = 0, M = 1, channels = 1;
+    std::vector<unsigned char> taps;   // original order (host copy for coefficients / design queries)
+    std::vector<unsigned char> scale;  // one Coef
+    DevBuf d_taps_rev;                 // cr[i] = h[L-1-i]  (DotProduct REVERSE, dot_product/mod.rs:73-81)
+    DevBuf d_hist[2];                  // [channels][L-1] oldest first
+    int cur = 0;
+    size_t ci = 0;                     // DecimatingFIRFilter::current_item (decim.rs:7)
+    int algo = SDSP_ALGO_AUTO;
+    hipStream_t stream = nullptr;
+    DevBuf stage_in, stage_out;
+    // overlap-save plan
+    bool ols_ok = false;
+    OlsPlan ols{};
+    DevBuf d_H, d_tw1, d_tw2;
+};
+
+namespace {
+
+int fir_alloc_state(sdsp_fir* h) {
+    const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
+    for (int i = 0; i < 2; ++i) {
+        SDSP_TRY(h->d_hist[i].ensure(hb), "alloc history");
+        if (hb) SDSP_TRY(hipMemsetAsync(h->d_hist[i].p, 0, hb, h->stream), "zero history");
+    }
+    h->cur = 0;
+    h->ci = 0;
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+bool ols_applicable(const sdsp_fir* h) {
+    return (h->dtype == SDSP_RC32 || h->dtype == SDSP_CC32) && h->M == 1 && h->L >= 2 && h->L - 1 <= 256 * 15;
+}
+
+// spectrum of g[i] = scale * h[L-1-i] in the lane layout of kern_fir_ols.hip
+int ols_build(sdsp_fir* h) {
+    const int N = kOlsN;
+    const size_t L = h->L;
+    const int h2 = (int)((L - 1 + 255) / 256);
+    std::vector<cd> g(N, cd{0.0, 0.0});
+    const cd s = coef_at(h->scale.data(), h->dtype, 0);
+    for (size_t i = 0; i < L; ++i) {
+        cd c = coef_at(h->taps.data(), h->dtype, L - 1 - i);
+        g[i] = coef_is_complex(h->dtype) ? cmul(c, s) : cd{c.re * s.re, c.re * s.im};
+    }
+    // direct DFT in f64 (one-time, O(N L))
+    std::vector<cd> G(N);
+    const double w = -2.0 * M_PI / N;
+    for (int k = 0; k < N; ++k) {
+        double re = 0.0, im = 0.0;
+        for (size_t i = 0; i < L; ++i) {
+            const long long ph = ((long long)i * k) % N;
+            const double c = std::cos(w * (double)ph), sn = std::sin(w * (double)ph);
+            re += g[i].re * c - g[i].im * sn;
+            im += g[i].re * sn + g[i].im * c;
+        }
+        G[k] = {re / N, im / N};
+    }
+    std::vector<float> Hs(2 * 4096), tw1(2 * 4096), tw2(2 * 256);
+    for (int t = 0; t < 256; ++t) {
+        const int k0 = t >> 4, k1 = t & 15;
+        for (int k2 = 0; k2 < 16; ++k2) {
+            const cd v = G[k0 + 16 * k1 + 256 * k2];
+            Hs[2 * (t * 16 + k2)] = (float)v.re;
+            Hs[2 * (t * 16 + k2) + 1] = (float)v.im;
+        }
+        for (int k = 0; k < 16; ++k) {
+            const long long ph = ((long long)t * k) % 4096;
+            tw1[2 * (t * 16 + k)] = (float)std::cos(-2.0 * M_PI * ph / 4096.0);
+            tw1[2 * (t * 16 + k) + 1] = (float)std::sin(-2.0 * M_PI * ph / 4096.0);
+        }
+    }
+    for (int a = 0; a < 16; ++a)
+        for (int b = 0; b < 16; ++b) {
+            const int ph = (a * b) % 256;
+            tw2[2 * (a * 16 + b)] = (float)std::cos(-2.0 * M_PI * ph / 256.0);
+            tw2[2 * (a * 16 + b) + 1] = (float)std::sin(-2.0 * M_PI * ph / 256.0);
+        }
+    SDSP_TRY(h->d_H.ensure(Hs.size() * 4), "alloc H");
+    SDSP_TRY(h->d_tw1.ensure(tw1.size() * 4), "alloc tw1");
+    SDSP_TRY(h->d_tw2.ensure(tw2.size() * 4), "alloc tw2");
+    SDSP_TRY(hipMemcpyAsync(h->d_H.p, Hs.data(), Hs.size() * 4, hipMemcpyHostToDevice, h->stream), "copy H");
+    SDSP_TRY(hipMemcpyAsync(h->d_tw1.p, tw1.data(), tw1.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw1");
+    SDSP_TRY(hipMemcpyAsync(h->d_tw2.p, tw2.data(), tw2.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw2");
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    h->ols = OlsPlan{h->d_H.p, h->d_tw1.p, h->d_tw2.p, h2};
+    h->ols_ok = true;
+    return SDSP_OK;
+}
+
+int fir_resolve_algo(const sdsp_fir* h, size_t n) {
+    if (h->algo == SDSP_ALGO_FFT) return ols_applicable(h) ? SDSP_ALGO_FFT : SDSP_ALGO_EXACT;
+    if (h->algo != SDSP_ALGO_AUTO) return h->algo;
+    // AUTO: overlap-save for long 32-bit complex blocks, reference-order direct form otherwise
+    if (ols_applicable(h) && n >= (size_t)(1 << 16)) return SDSP_ALGO_FFT;
+    return SDSP_ALGO_EXACT;
+}
+
+int fir_create_common(sdsp_fir** out, int dtype, const void* taps, size_t len, const void* scale, size_t M,
+                      int device) {
+    *out = nullptr;
+    if (dtype < 0 || dtype > 5) {
+        set_error("bad dtype");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    if (len == 0) {
+        set_error("FIR Filter Error CoefficientsLengthZero");
+        return SDSP_E_COEFFICIENTS_LENGTH_ZERO;
+    }
+    if (M < 1) {
+        set_error("FIR Filter Error DecimationLessThanOne");
+        return SDSP_E_DECIMATION_LESS_THAN_ONE;
+    }
+    if (len > (1u << 30)) {
+        set_error("tap count too large");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    DeviceInfo info;
+    int st = check_device(device, &info);
+    if (st) return st;
+    DeviceGuard g(device);
+    sdsp_fir* h = new sdsp_fir();
+    h->dtype = dtype;
+    h->device = device;
+    h->cus = info.cus;
+    h->L = len;
+    h->M = M;
+    const size_t cb = coef_bytes(dtype);
+    h->taps.assign((const unsigned char*)taps, (const unsigned char*)taps + len * cb);
+    h->scale.assign((const unsigned char*)scale, (const unsigned char*)scale + cb);
+    std::vector<unsigned char> rev(len * cb);
+    for (size_t i = 0; i < len; ++i) std::memcpy(&rev[i * cb], &h->taps[(len - 1 - i) * cb], cb);
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = h->d_taps_rev.ensure(rev.size());
+    if (e == hipSuccess) e = hipMemcpy(h->d_taps_rev.p, rev.data(), rev.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        st = device_status(e, "fir create");
+        sdsp_fir_destroy(h);
+        return st;
+    }
+    st = fir_alloc_state(h);
+    if (st) {
+        sdsp_fir_destroy(h);
+        return st;
+    }
+    *out = h;
+    return SDSP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sdsp_last_error(void) { return g_last_error.c_str(); }
+const char* sdsp_version(void) { return "sdsp 0.1.0 (gfx950)"; }
+size_t sdsp_sample_size(int dtype) { return sample_bytes(dtype); }
+size_t sdsp_coef_size(int dtype) { return coef_bytes(dtype); }
+
+int sdsp_device_count(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) return 0;
+    int n = 0;
+    for (int d = 0; d < count; ++d) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, d) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0) ++n;
+    }
+    return n;
+}
+
+int sdsp_fir_create(sdsp_fir** out, int dtype, const void* taps, size_t len, const void* scale, int device) {
+    return fir_create_common(out, dtype, taps, len, scale, 1, device);
+}
+
+int sdsp_decim_create(sdsp_fir** out, int dtype, const void* taps, size_t len, const void* scale,
+                      size_t decimation, int device) {
+    return fir_create_common(out, dtype, taps, len, scale, decimation, device);
+}
+
+void sdsp_fir_destroy(sdsp_fir* h) {
+    if (!h) return;
+    {
+        DeviceGuard g(h->device);
+        if (h->stream) {
+            (void)hipStreamSynchronize(h->stream);
+            (void)hipStreamDestroy(h->stream);
+        }
+        h->d_taps_rev.release();
+        h->d_hist[0].release();
+        h->d_hist[1].release();
+        h->stage_in.release();
+        h->stage_out.release();
+        h->d_H.release();
+        h->d_tw1.release();
+        h->d_tw2.release();
+    }
+    delete h;
+}
+
+int sdsp_fir_set_channels(sdsp_fir* h, size_t channels) {
+    if (!h || channels == 0) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    h->channels = channels;
+    return fir_alloc_state(h);
+}
+
+int sdsp_fir_set_algo(sdsp_fir* h, int algo) {
+    if (!h || algo < 0 || algo > 3) return SDSP_E_INVALID_ARGUMENT;
+    if (algo == SDSP_ALGO_FFT && !ols_applicable(h)) {
+        set_error("overlap-save needs 32-bit complex samples, no decimation and L-1 <= 3840");
+        return SDSP_E_UNSUPPORTED;
+    }
+    h->algo = algo;
+    return SDSP_OK;
+}
+
+int sdsp_fir_get_algo(const sdsp_fir* h) { return h ? h->algo : -1; }
+
+int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out) {
+    if (!h || !out) return SDSP_E_INVALID_ARGUMENT;
+    int st = fir_create_common(out, h->dtype, h->taps.data(), h->L, h->scale.data(), h->M, h->device);
+    if (st) return st;
+    sdsp_fir* c = *out;
+    DeviceGuard g(h->device);
+    c->algo = h->algo;
+    if (h->channels != 1) {
+        st = sdsp_fir_set_channels(c, h->channels);
+        if (st) return st;
+    }
+    const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    if (hb) SDSP_TRY(hipMemcpy(c->d_hist[0].p, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToDevice), "clone state");
+    c->cur = 0;
+    c->ci = h->ci;
+    return SDSP_OK;
+}
+
+int sdsp_fir_set_scale(sdsp_fir* h, const void* scale) {
+    if (!h || !scale) return SDSP_E_INVALID_ARGUMENT;
+    std::memcpy(h->scale.data(), scale, h->scale.size());
+    h->ols_ok = false;
+    return SDSP_OK;
+}
+int sdsp_fir_get_scale(const sdsp_fir* h, void* scale) {
+    if (!h || !scale) return SDSP_E_INVALID_ARGUMENT;
+    std::memcpy(scale, h->scale.data(), h->scale.size());
+    return SDSP_OK;
+}
+size_t sdsp_fir_len(const sdsp_fir* h) { return h ? h->L : 0; }
+size_t sdsp_fir_decimation(const sdsp_fir* h) { return h ? h->M : 0; }
+
+int sdsp_fir_coefficients(const sdsp_fir* h, void* out) {
+    if (!h || !out) return SDSP_E_INVALID_ARGUMENT;
+    const size_t cb = coef_bytes(h->dtype);
+    unsigned char* o = (unsigned char*)out;
+    for (size_t i = 0; i < h->L; ++i) std::memcpy(o + i * cb, &h->taps[(h->L - 1 - i) * cb], cb);
+    return SDSP_OK;
+}
+
+size_t sdsp_fir_output_count(const sdsp_fir* h, size_t n) {
+    if (!h) return 0;
+    if (h->M == 1) return n;
+    const size_t j0 = (h->M - 1 - h->ci) % h->M;  // first input index whose push wraps the phase to 0
+    return j0 < n ? (n - 1 - j0) / h->M + 1 : 0;
+}
+
+int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void* d_out, size_t* n_out,
+                                  void* stream) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    hipStream_t s = pick(stream, h->stream);
+    const size_t nout = sdsp_fir_output_count(h, n);
+    if (n_out) *n_out = nout;
+    if (n == 0) return SDSP_OK;
+    const void* hist = h->d_hist[h->cur].p;
+    if (h->M == 1) {
+        const int algo = fir_resolve_algo(h, n);
+        if (algo == SDSP_ALGO_FFT) {
+            if (!h->ols_ok) {
+                int st = ols_build(h);
+                if (st) return st;
+            }
+            SDSP_TRY(launch_fir_ols(h->ols, d_in, hist, d_out, n, (int)h->L, h->channels, h->cus, s), "fir ols");
+        } else {
+            FirArgs a{d_in, hist, h->d_taps_rev.p, h->scale.data(), d_out, n, n, h->channels, (int)h->L, 1, 0,
+                      algo != SDSP_ALGO_FMA};
+            SDSP_TRY(launch_fir_direct(h->dtype, a, s), "fir direct");
+        }
+    } else {
+        const size_t j0 = (h->M - 1 - h->ci) % h->M;
+        const int algo = h->algo == SDSP_ALGO_FMA ? SDSP_ALGO_FMA : SDSP_ALGO_EXACT;
+        FirArgs a{d_in, hist, h->d_taps_rev.p, h->scale.data(), d_out, n, nout, h->channels, (int)h->L, (int)h->M,
+                  j0, algo != SDSP_ALGO_FMA};
+        SDSP_TRY(launch_decim_direct(h->dtype, a, s), "decim direct");
+        h->ci = (h->ci + n) % h->M;
+    }
+    SDSP_TRY(launch_hist_update(h->dtype, d_in, hist, h->d_hist[h->cur ^ 1].p, n, (int)h->L - 1, h->channels, s),
+             "history update");
+    h->cur ^= 1;
+    return SDSP_OK;
+}
+
+int sdsp_fir_execute_block(sdsp_fir* h, const void* in, size_t n, void* out, size_t* n_out) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    const size_t sb = sample_bytes(h->dtype);
+    const size_t nout = sdsp_fir_output_count(h, n);
+    if (n_out) *n_out = nout;
+    if (n == 0) return SDSP_OK;
+    SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
+    SDSP_TRY(h->stage_out.ensure(h->channels * std::max<size_t>(nout, 1) * sb), "stage out");
+    SDSP_TRY(hipMemcpyAsync(h->stage_in.p, in, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
+    int st = sdsp_fir_execute_block_device(h, h->stage_in.p, n, h->stage_out.p, nullptr, h->stream);
+    if (st) return st;
+    if (nout)
+        SDSP_TRY(hipMemcpyAsync(out, h->stage_out.p, h->channels * nout * sb, hipMemcpyDeviceToHost, h->stream),
+                 "D2H");
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_fir_execute(sdsp_fir* h, const void* sample, void* out, size_t* n_out) {
+    if (!h || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
+    return sdsp_fir_execute_block(h, sample, 1, out, n_out);
+}
+
+int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) return SDSP_OK;
+    DeviceGuard g(h->device);
+    const size_t sb = sample_bytes(h->dtype);
+    SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
+    SDSP_TRY(hipMemcpyAsync(h->stage_in.p, samples, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
+    SDSP_TRY(launch_hist_update(h->dtype, h->stage_in.p, h->d_hist[h->cur].p, h->d_hist[h->cur ^ 1].p, n,
+                                (int)h->L - 1, h->channels, h->stream),
+             "history update");
+    h->cur ^= 1;
+    h->ci = (h->ci + n) % h->M;
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_decim_push(sdsp_fir* h, const void* sample) { return sdsp_decim_write(h, sample, 1); }
+
+int sdsp_fir_reset(sdsp_fir* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    return fir_alloc_state(h);
+}
+
+size_t sdsp_fir_state_len(const sdsp_fir* h) { return h ? h->channels * (h->L - 1) : 0; }
+
+int sdsp_fir_get_state(const sdsp_fir* h, void* hist, size_t* phase) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    if (hb && hist) SDSP_TRY(hipMemcpy(hist, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToHost), "get state");
+    if (phase) *phase = h->ci;
+    return SDSP_OK;
+}
+
+int sdsp_fir_set_state(sdsp_fir* h, const void* hist, size_t phase) {
+    if (!h || phase >= h->M) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    if (hb && hist) SDSP_TRY(hipMemcpy(h->d_hist[h->cur].p, hist, hb, hipMemcpyHostToDevice), "set state");
+    h->ci = phase;
+    return SDSP_OK;
+}
+
+int sdsp_fir_frequency_response(const sdsp_fir* h, double f, double* re_im) {
+    if (!h || !re_im) return SDSP_E_INVALID_ARGUMENT;
+    // coefficients() returns the REVERSED stored taps (fir/mod.rs:173-176, used at :263-273)
+    std::vector<cd> c(h->L);
+    for (size_t i = 0; i < h->L; ++i) c[i] = coef_at(h->taps.data(), h->dtype, h->L - 1 - i);
+    const bool real = !coef_is_complex(h->dtype);
+    cd o = poly_response(c, real, f);
+    cd s = coef_at(h->scale.data(), h->dtype, 0);
+    cd r = real ? cmul(s.re, o) : cmul(s, o);
+    re_im[0] = r.re;
+    re_im[1] = r.im;
+    return SDSP_OK;
+}
+
+int sdsp_fir_group_delay(const sdsp_fir* h, double f, double* delay) {
+    if (!h || !delay) return SDSP_E_INVALID_ARGUMENT;
+    std::vector<cd> c(h->L);
+    for (size_t i = 0; i < h->L; ++i) c[i] = coef_at(h->taps.data(), h->dtype, h->L - 1 - i);
+    double d = 0.0;
+    if (fir_group_delay(c, !coef_is_complex(h->dtype), f, &d)) d = 0.0;  // errors map to 0.0 (:293-303)
+    *delay = d;
+    return SDSP_OK;
+}
+
+int sdsp_fir_synchronize(sdsp_fir* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Polyphase filterbank / interpolating FIR
+// ===========================================================================
+struct sdsp_pfb {
+    int dtype = 0, device = 0;
+    size_t M = 0, K = 0, channels = 1;
+    bool interp = false;
+    std::vector<unsigned char> cb;     // [M][K] branch coefficients, stored order
+    std::vector<unsigned char> scale;  // kept, never applied (pfb.rs:85-90)
+    DevBuf d_cb;
+    DevBuf d_hist[2];  // [channels][K] : the Window(K), oldest first
+    int cur = 0;
+    int algo = SDSP_ALGO_EXACT;
+    hipStream_t stream = nullptr;
+    DevBuf stage_in, stage_out;
+};
+
+namespace {
+
+int pfb_alloc_state(sdsp_pfb* h) {
+    const size_t hb = h->channels * h->K * sample_bytes(h->dtype);
+    for (int i = 0; i < 2; ++i) {
+        SDSP_TRY(h->d_hist[i].ensure(hb), "alloc window");
+        SDSP_TRY(hipMemsetAsync(h->d_hist[i].p, 0, hb, h->stream), "zero window");
+    }
+    h->cur = 0;
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int pfb_create_common(sdsp_pfb** out, int dtype, const unsigned char* taps, size_t len, size_t M,
+                      const unsigned char* scale, bool interp, int device) {
+    *out = nullptr;
+    const size_t cbytes = coef_bytes(dtype);
+    const size_t K = len / M;
+    if (K == 0) {  // the reference panics in Window::new(0) (src/window/mod.rs:18)
+        set_error("fewer taps than filters: sub-filter length 0");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    DeviceInfo info;
+    int st = check_device(device, &info);
+    if (st) return st;
+    DeviceGuard g(device);
+    sdsp_pfb* h = new sdsp_pfb();
+    h->dtype = dtype;
+    h->device = device;
+    h->M = M;
+    h->K = K;
+    h->interp = interp;
+    h->scale.assign(scale, scale + cbytes);
+    h->cb.resize(M * K * cbytes);
+    // rev_sub_coefs[K - index - 1] = coefficients[filter + index * filters]  (pfb.rs:33-40)
+    for (size_t p = 0; p < M; ++p)
+        for (size_t idx = 0; idx < K; ++idx)
+            std::memcpy(&h->cb[(p * K + (K - idx - 1)) * cbytes], taps + (p + idx * M) * cbytes, cbytes);
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = h->d_cb.ensure(h->cb.size());
+    if (e == hipSuccess) e = hipMemcpy(h->d_cb.p, h->cb.data(), h->cb.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        st = device_status(e, "pfb create");
+        sdsp_pfb_destroy(h);
+        return st;
+    }
+    st = pfb_alloc_state(h);
+    if (st) {
+        sdsp_pfb_destroy(h);
+        return st;
+    }
+    *out = h;
+    return SDSP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdsp_pfb_create(sdsp_pfb** out, int dtype, const void* taps, size_t len, size_t filters, const void* scale,
+                    int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (dtype < 0 || dtype > 5) return SDSP_E_INVALID_ARGUMENT;
+    if (filters == 0) {  // pfb.rs:25-26
+        set_error("FIR Filter Error NotEnoughFilters");
+        return SDSP_E_NOT_ENOUGH_FILTERS;
+    }
+    if (len == 0) {  // pfb.rs:27-28
+        set_error("FIR Filter Error CoefficientsLengthZero");
+        return SDSP_E_COEFFICIENTS_LENGTH_ZERO;
+    }
+    return pfb_create_common(out, dtype, (const unsigned char*)taps, len, filters, (const unsigned char*)scale,
+                             false, device);
+}
+
+int sdsp_interp_create(sdsp_pfb** out, int dtype, const void* taps, size_t len, size_t M, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (dtype < 0 || dtype > 5) return SDSP_E_INVALID_ARGUMENT;
+    if (len == 0) {  // interp.rs:28-29
+        set_error("FIR Filter Error CoefficientsLengthZero");
+        return SDSP_E_COEFFICIENTS_LENGTH_ZERO;
+    }
+    if (M < 1) {  // interp.rs:30-31
+        set_error("FIR Filter Error InterpolationLessThanOne");
+        return SDSP_E_INTERPOLATION_LESS_THAN_ONE;
+    }
+    // sub-filter length computed in f32 (interp.rs:35-40), taps zero-padded to K*M (:43-46)
+    const float q = (float)len / (float)M;
+    const size_t K = (q == std::floor(q)) ? (size_t)q : (size_t)std::ceil(q);
+    const size_t cbytes = coef_bytes(dtype);
+    std::vector<unsigned char> eff(K * M * cbytes, 0);
+    std::memcpy(eff.data(), taps, std::min(len, K * M) * cbytes);
+    std::vector<unsigned char> one(cbytes, 0);
+    if (coef_is_f32(dtype)) { float v = 1.0f; std::memcpy(one.data(), &v, 4); }
+    else { double v = 1.0; std::memcpy(one.data(), &v, 8); }
+    return pfb_create_common(out, dtype, eff.data(), K * M, M, one.data(), true, device);
+}
+
+void sdsp_pfb_destroy(sdsp_pfb* h) {
+    if (!h) return;
+    {
+        DeviceGuard g(h->device);
+        if (h->stream) {
+            (void)hipStreamSynchronize(h->stream);
+            (void)hipStreamDestroy(h->stream);
+        }
+        h->d_cb.release();
+        h->d_hist[0].release();
+        h->d_hist[1].release();
+        h->stage_in.release();
+        h->stage_out.release();
+    }
+    delete h;
+}
+
+int sdsp_pfb_clone(const sdsp_pfb* h, sdsp_pfb** out) {
+    if (!h || !out) return SDSP_E_INVALID_ARGUMENT;
+    DeviceInfo info;
+    int st = check_device(h->device, &info);
+    if (st) return st;
+    DeviceGuard g(h->device);
+    sdsp_pfb* c = new sdsp_pfb();
+    c->dtype = h->dtype; c->device = h->device; c->M = h->M; c->K = h->K; c->channels = h->channels;
+    c->interp = h->interp; c->cb = h->cb; c->scale = h->scale; c->algo = h->algo;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = c->d_cb.ensure(c->cb.size());
+    if (e == hipSuccess) e = hipMemcpy(c->d_cb.p, c->cb.data(), c->cb.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { st = device_status(e, "pfb clone"); sdsp_pfb_destroy(c); return st; }
+    st = pfb_alloc_state(c);
+    if (st) { sdsp_pfb_destroy(c); return st; }
+    const size_t hb = h->channels * h->K * sample_bytes(h->dtype);
+    e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipMemcpy(c->d_hist[0].p, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToDevice);
+    if (e != hipSuccess) { st = device_status(e, "pfb clone state"); sdsp_pfb_destroy(c); return st; }
+    *out = c;
+    return SDSP_OK;
+}
+
+size_t sdsp_pfb_len(const sdsp_pfb* h) { return h ? h->M : 0; }
+size_t sdsp_pfb_subfilter_len(const sdsp_pfb* h) { return h ? h->K : 0; }
+int sdsp_pfb_set_scale(sdsp_pfb* h, const void* scale) {
+    if (!h || !scale) return SDSP_E_INVALID_ARGUMENT;
+    std::memcpy(h->scale.data(), scale, h->scale.size());
+    return SDSP_OK;
+}
+int sdsp_pfb_get_scale(const sdsp_pfb* h, void* scale) {
+    if (!h || !scale) return SDSP_E_INVALID_ARGUMENT;
+    std::memcpy(scale, h->scale.data(), h->scale.size());
+    return SDSP_OK;
+}
+int sdsp_pfb_coefficients(const sdsp_pfb* h, void* out) {
+    if (!h || !out) return SDSP_E_INVALID_ARGUMENT;
+    std::memcpy(out, h->cb.data(), h->cb.size());
+    return SDSP_OK;
+}
+
+int sdsp_pfb_execute_block_device(sdsp_pfb* h, const void* d_in, size_t n, void* d_out, void* stream) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) return SDSP_OK;
+    DeviceGuard g(h->device);
+    hipStream_t s = pick(stream, h->stream);
+    PfbArgs a{d_in, h->d_hist[h->cur].p, h->d_cb.p, d_out, n, h->channels, (int)h->K, (int)h->M, (int)h->K,
+              h->algo != SDSP_ALGO_FMA};
+    SDSP_TRY(launch_pfb(h->dtype, a, s), "pfb");
+    SDSP_TRY(launch_hist_update(h->dtype, d_in, h->d_hist[h->cur].p, h->d_hist[h->cur ^ 1].p, n, (int)h->K,
+                                h->channels, s),
+             "window update");
+    h->cur ^= 1;
+    return SDSP_OK;
+}
+
+int sdsp_pfb_execute_block(sdsp_pfb* h, const void* in, size_t n, void* out) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) return SDSP_OK;
+    DeviceGuard g(h->device);
+    const size_t sb = sample_bytes(h->dtype);
+    SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
+    SDSP_TRY(h->stage_out.ensure(h->channels * n * h->M * sb), "stage out");
+    SDSP_TRY(hipMemcpyAsync(h->stage_in.p, in, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
+    int st = sdsp_pfb_execute_block_device(h, h->stage_in.p, n, h->stage_out.p, h->stream);
+    if (st) return st;
+    SDSP_TRY(hipMemcpyAsync(out, h->stage_out.p, h->channels * n * h->M * sb, hipMemcpyDeviceToHost, h->stream),
+             "D2H");
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_pfb_push(sdsp_pfb* h, const void* sample) {
+    if (!h || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    const size_t sb = sample_bytes(h->dtype);
+    SDSP_TRY(h->stage_in.ensure(sb), "stage in");
+    SDSP_TRY(hipMemcpyAsync(h->stage_in.p, sample, sb, hipMemcpyHostToDevice, h->stream), "H2D");
+    SDSP_TRY(launch_hist_update(h->dtype, h->stage_in.p, h->d_hist[h->cur].p, h->d_hist[h->cur ^ 1].p, 1,
+                                (int)h->K, 1, h->stream),
+             "window push");
+    h->cur ^= 1;
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_pfb_execute(sdsp_pfb* h, size_t index, void* out) {
+    if (!h || h->channels != 1 || index >= h->M) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    const size_t sb = sample_bytes(h->dtype);
+    SDSP_TRY(h->stage_out.ensure(h->M * sb), "stage out");
+    // all branches on the current window: x = newest sample, history = the K-1 before it
+    const unsigned char* win = (const unsigned char*)h->d_hist[h->cur].p;
+    PfbArgs a{win + (h->K - 1) * sb, win, h->d_cb.p, h->stage_out.p, 1, 1, (int)h->K, (int)h->M,
+              (int)h->K - 1, h->algo != SDSP_ALGO_FMA};
+    SDSP_TRY(launch_pfb(h->dtype, a, h->stream), "pfb execute");
+    SDSP_TRY(hipMemcpyAsync(out, (unsigned char*)h->stage_out.p + index * sb, sb, hipMemcpyDeviceToHost, h->stream),
+             "D2H");
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_pfb_reset(sdsp_pfb* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    return pfb_alloc_state(h);
+}
+
+// InterpolatingFIRFilter::frequency_response / group_delay over the flattened
+// branch coefficients (interp.rs:113-137); PolyPhaseFilterBank has no Filter impl.
+int sdsp_pfb_frequency_response(const sdsp_pfb* h, double f, double* re_im) {
+    if (!h || !re_im) return SDSP_E_INVALID_ARGUMENT;
+    std::vector<cd> c(h->M * h->K);
+    for (size_t i = 0; i < c.size(); ++i) c[i] = coef_at(h->cb.data(), h->dtype, i);
+    const bool real = !coef_is_complex(h->dtype);
+    cd o = poly_response(c, real, f);
+    cd s = coef_at(h->scale.data(), h->dtype, 0);
+    cd r = real ? cmul(s.re, o) : cmul(s, o);
+    re_im[0] = r.re;
+    re_im[1] = r.im;
+    return SDSP_OK;
+}
+
+int sdsp_pfb_group_delay(const sdsp_pfb* h, double f, double* delay) {
+    if (!h || !delay) return SDSP_E_INVALID_ARGUMENT;
+    std::vector<cd> c(h->M * h->K);
+    for (size_t i = 0; i < c.size(); ++i) c[i] = coef_at(h->cb.data(), h->dtype, i);
+    double d = 0.0;
+    if (fir_group_delay(c, !coef_is_complex(h->dtype), f, &d)) d = 0.0;
+    *delay = d;
+    return SDSP_OK;
+}
+
+int sdsp_pfb_synchronize(sdsp_pfb* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+// ===========================================================================
+// utilities
+// ===========================================================================
+int sdsp_synth_f32_device(void* d_out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,
+                          void* stream) {
+    SDSP_TRY(launch_synth_f32((float*)d_out, seed, channel, start, count, (hipStream_t)stream), "synth");
+    return SDSP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// Device-side arithmetic for the sdsp kernels (gfx950).
+//
+// Every kernel TU is compiled with -ffp-contract=off, so `a * b + c` is a
+// rounded multiply followed by a rounded add — the arithmetic the reference's
+// Rust code performs (num-complex 0.4 Mul/Add, src/dot_product/mod.rs:159-170).
+// Fused multiply-add is only ever requested explicitly (fmac below).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sdsp {
+
+template <typename T> struct cpx {
+    T re, im;
+};
+using c32 = cpx<float>;
+using c64 = cpx<double>;
+
+template <typename T> struct is_cpx { static constexpr bool value = false; };
+template <typename T> struct is_cpx<cpx<T>> { static constexpr bool value = true; };
+template <typename T> struct real_of { using type = T; };
+template <typename T> struct real_of<cpx<T>> { using type = T; };
+
+template <typename T> __host__ __device__ inline T zero_v() { return T(0); }
+template <> __host__ __device__ inline c32 zero_v<c32>() { return {0.0f, 0.0f}; }
+template <> __host__ __device__ inline c64 zero_v<c64>() { return {0.0, 0.0}; }
+
+// ---- num-complex semantics (no contraction: TU built with -ffp-contract=off)
+__device__ inline float mul_(float a, float b) { return a * b; }
+__device__ inline double mul_(double a, double b) { return a * b; }
+template <typename T> __device__ inline cpx<T> mul_(T a, cpx<T> b) { return {a * b.re, a * b.im}; }
+template <typename T> __device__ inline cpx<T> mul_(cpx<T> a, T b) { return {a.re * b, a.im * b}; }
+template <typename T> __device__ inline cpx<T> mul_(cpx<T> a, cpx<T> b) {
+    T re = a.re * b.re - a.im * b.im;
+    T im = a.re * b.im + a.im * b.re;
+    return {re, im};
+}
+__device__ inline float add_(float a, float b) { return a + b; }
+__device__ inline double add_(double a, double b) { return a + b; }
+template <typename T> __device__ inline cpx<T> add_(cpx<T> a, cpx<T> b) { return {a.re + b.re, a.im + b.im}; }
+__device__ inline float sub_(float a, float b) { return a - b; }
+__device__ inline double sub_(double a, double b) { return a - b; }
+template <typename T> __device__ inline cpx<T> sub_(cpx<T> a, cpx<T> b) { return {a.re - b.re, a.im - b.im}; }
+
+// ---- fused variants: acc + c * s with one rounding per fma
+__device__ inline float fmac_(float acc, float c, float s) { return __builtin_fmaf(c, s, acc); }
+__device__ inline double fmac_(double acc, double c, double s) { return __builtin_fma(c, s, acc); }
+template <typename T> __device__ inline cpx<T> fmac_(cpx<T> acc, T c, cpx<T> s) {
+    return {fmac_(acc.re, c, s.re), fmac_(acc.im, c, s.im)};
+}
+template <typename T> __device__ inline cpx<T> fmac_(cpx<T> acc, cpx<T> c, cpx<T> s) {
+    T re = fmac_(fmac_(acc.re, c.re, s.re), -c.im, s.im);
+    T im = fmac_(fmac_(acc.im, c.re, s.im), c.im, s.re);
+    return {re, im};
+}
+
+// acc += c * s   in the reference order (EXACT) or fused
+template <bool EXACT, typename C, typename I, typename O>
+__device__ inline O mac(O acc, C c, I s) {
+    if constexpr (EXACT) return add_(acc, mul_(c, s));
+    else return fmac_(acc, c, s);
+}
+
+// Out type of Coef * In
+template <typename C, typename I> struct out_of { using type = I; };
+
+}  // namespace sdsp

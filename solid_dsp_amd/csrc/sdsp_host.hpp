@@ -1,0 +1,73 @@
+// Internal host-side helpers shared by runtime.cpp and design.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace sdsp {
+
+struct cd { double re, im; };
+
+cd cmul(cd a, cd b);
+cd cmul(double a, cd b);
+cd cadd(cd a, cd b);
+cd cdiv(cd a, cd b);
+cd from_polar(double r, double t);
+cd poly_response(const std::vector<cd>& c, bool real, double f);
+int fir_group_delay(const std::vector<cd>& h, bool real, double f, double* out);
+int iir_group_delay(const std::vector<double>& b, const std::vector<double>& a, double f, double* out);
+
+void set_error(const std::string& msg);
+int device_status(hipError_t e, const char* what);
+
+// dtype traits (sdsp_dtype)
+inline size_t sample_bytes(int dt) {
+    static const size_t b[6] = {4, 8, 8, 8, 16, 16};
+    return (dt >= 0 && dt < 6) ? b[dt] : 0;
+}
+inline size_t coef_bytes(int dt) {
+    static const size_t b[6] = {4, 4, 8, 8, 8, 16};
+    return (dt >= 0 && dt < 6) ? b[dt] : 0;
+}
+inline bool coef_is_complex(int dt) { return dt == 2 || dt == 5; }
+inline bool coef_is_f32(int dt) { return dt <= 2; }
+
+// widen one stored coefficient to complex<f64>
+inline cd coef_at(const unsigned char* p, int dt, size_t i) {
+    switch (dt) {
+        case 0: case 1: { float v; std::memcpy(&v, p + 4 * i, 4); return {(double)v, 0.0}; }
+        case 2: { float v[2]; std::memcpy(v, p + 8 * i, 8); return {(double)v[0], (double)v[1]}; }
+        case 3: case 4: { double v; std::memcpy(&v, p + 8 * i, 8); return {v, 0.0}; }
+        case 5: { double v[2]; std::memcpy(v, p + 16 * i, 16); return {v[0], v[1]}; }
+    }
+    return {0.0, 0.0};
+}
+
+// owned device allocation
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t ensure(size_t b) {
+        if (b <= bytes && p) return hipSuccess;
+        release();
+        if (b == 0) b = 16;
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipSuccess) bytes = b;
+        else p = nullptr;
+        return e;
+    }
+};
+
+}  // namespace sdsp

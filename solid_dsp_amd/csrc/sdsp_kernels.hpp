@@ -1,0 +1,53 @@
+// Internal launcher interface between the C-ABI runtime (runtime.cpp) and the
+// kernel translation units.  Not installed; no torch types anywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sdsp {
+
+struct FirArgs {
+    const void* x;         // device input, channel-major [channels][n]
+    const void* hist;      // device history [channels][L-1], oldest first
+    const void* taps_rev;  // device reversed taps cr[i] = h[L-1-i]
+    const void* scale;     // host pointer to one Coef
+    void* y;               // device output [channels][nout]
+    size_t n, nout, channels;
+    int L, M;
+    size_t j0;             // block-relative index of the first emitting input (decimator)
+    bool exact;
+};
+
+hipError_t launch_fir_direct(int dtype, const FirArgs& a, hipStream_t s);
+hipError_t launch_decim_direct(int dtype, const FirArgs& a, hipStream_t s);
+hipError_t launch_hist_update(int dtype, const void* x, const void* old_hist, void* new_hist, size_t n, int Lm1,
+                              size_t channels, hipStream_t s);
+
+// overlap-save (N = 4096) for 32-bit complex samples
+struct OlsPlan {
+    void* d_H;    // [256][16] c32: H[k0 + 16 k1 + 256 k2] / N * scale, row t = 16 k0 + k1
+    void* d_tw1;  // [256][16] c32: W4096^(t*k)
+    void* d_tw2;  // [16][16]  c32: W256^(a*b)
+    int halo_rows;  // h2: halo = 256*h2 >= L-1
+};
+constexpr int kOlsN = 4096;
+hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
+                          size_t channels, int num_cus, hipStream_t s);
+
+// polyphase filterbank / interpolator: out[j*M + p] = sum_{i<K} cb[p*K + i] * ext(j - i)
+struct PfbArgs {
+    const void* x;
+    const void* hist;  // [channels][H] oldest first; ext(j<0) = hist[H + j]
+    const void* cb;    // device branch coefs [M][K] (stored order, pfb.rs:33-40)
+    void* y;           // [channels][n*M]
+    size_t n, channels;
+    int K, M, H;
+    bool exact;
+};
+hipError_t launch_pfb(int dtype, const PfbArgs& a, hipStream_t s);
+
+hipError_t launch_synth_f32(float* out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,
+                            hipStream_t s);
+
+}  // namespace sdsp

@@ -1,0 +1,243 @@
+"""ctypes loader for the CPU restatement in ``oracle/`` (test infrastructure only).
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg use
+this module; the product package ``solid_dsp_amd`` never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "_build", "libsdsp_oracle.so")
+
+RR32, RC32, CC32, RR64, RC64, CC64 = range(6)
+NORMAL, SECOND_ORDER = 0, 1
+
+_IN_DT = {RR32: np.float32, RC32: np.complex64, CC32: np.complex64,
+          RR64: np.float64, RC64: np.complex128, CC64: np.complex128}
+_COEF_DT = {RR32: np.float32, RC32: np.float32, CC32: np.complex64,
+            RR64: np.float64, RC64: np.float64, CC64: np.complex128}
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+    return ORACLE_SO
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(ORACLE_SO):
+        build()
+    L = C.CDLL(ORACLE_SO)
+    vp, sz, ip, dp = C.c_void_p, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_double)
+    sig = {
+        "orc_msb_index": (sz, [sz]),
+        "orc_fir_new": (vp, [C.c_int, vp, sz, vp, ip]),
+        "orc_decim_new": (vp, [C.c_int, vp, sz, vp, sz, ip]),
+        "orc_pfb_new": (vp, [C.c_int, vp, sz, sz, vp, ip]),
+        "orc_interp_new": (vp, [C.c_int, vp, sz, sz, ip]),
+        "orc_execute_block": (sz, [vp, vp, sz, vp]),
+        "orc_push": (None, [vp, vp]),
+        "orc_write": (None, [vp, vp, sz]),
+        "orc_reset": (None, [vp]),
+        "orc_clone": (vp, [vp]),
+        "orc_free": (None, [vp]),
+        "orc_group_delay": (C.c_double, [vp, C.c_double]),
+        "orc_frequency_response": (None, [vp, C.c_double, dp]),
+        "orc_pfb_execute": (C.c_int, [vp, C.c_int, sz, vp]),
+        "orc_iir_new": (vp, [C.c_int, vp, sz, vp, sz, C.c_int, ip]),
+        "orc_iir_decim_new": (vp, [C.c_int, vp, sz, vp, sz, C.c_int, sz, ip]),
+        "orc_iir_interp_new": (vp, [C.c_int, vp, sz, vp, sz, C.c_int, sz, ip]),
+        "orc_sos_new": (vp, [dp, sz, dp, sz, ip]),
+        "orc_sos_execute": (C.c_double, [vp, C.c_double]),
+        "orc_sos_group_delay": (C.c_double, [vp, C.c_double]),
+        "orc_sos_coefs": (None, [vp, dp, dp]),
+        "orc_sos_free": (None, [vp]),
+        "orc_dot_execute": (None, [C.c_int, vp, sz, C.c_int, vp, sz, dp]),
+        "orc_fir_group_delay": (C.c_double, [dp, sz, C.c_double, ip]),
+        "orc_iir_group_delay": (C.c_double, [dp, sz, dp, sz, C.c_double, ip]),
+        "orc_sinc": (C.c_double, [C.c_double]),
+        "orc_besseli": (C.c_double, [C.c_double, C.c_double]),
+        "orc_lngamma": (C.c_double, [C.c_double]),
+        "orc_kaiser": (C.c_double, [sz, sz, C.c_double]),
+        "orc_kaiser_beta": (C.c_double, [C.c_double]),
+        "orc_firdes_kaiser": (C.c_int, [sz, C.c_double, C.c_double, C.c_double, dp]),
+        "orc_firdes_notch": (C.c_int, [sz, C.c_double, C.c_double, dp]),
+        "orc_estimate_req_filter_len": (C.c_int, [C.c_double, C.c_double, C.c_int, C.POINTER(sz)]),
+        "orc_estimate_req_filter_as": (C.c_double, [C.c_double, sz, C.c_int]),
+        "orc_estimate_req_filter_df": (C.c_double, [C.c_double, sz, C.c_int]),
+        "orc_active_lag": (C.c_int, [C.c_double, C.c_double, C.c_double, dp, dp]),
+        "orc_active_pi": (C.c_int, [C.c_double, C.c_double, C.c_double, dp, dp]),
+        "orc_synth_f32": (None, [C.c_uint64, C.c_uint64, C.c_uint64, sz, C.POINTER(C.c_float)]),
+    }
+    optional = {
+        "orc_fft_new": (vp, [sz, C.c_int]),
+        "orc_fft_execute": (C.c_int, [vp, vp, vp]),
+        "orc_fft_free": (None, [vp]),
+        "orc_fft_method": (C.c_int, [vp]),
+        "orc_channelize": (sz, [vp, sz, sz, vp, sz, vp]),
+    }
+    for name, (res, args) in list(sig.items()) + list(optional.items()):
+        if not hasattr(L, name):
+            if name in optional:
+                continue
+            raise RuntimeError(f"oracle missing symbol {name}")
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _dptr(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class OracleObj:
+    """Generic wrapper over an oracle filter handle."""
+
+    def __init__(self, h, dtype, out_per_in=1, kind="fir", M=1):
+        self.h = h
+        self.dtype = dtype
+        self.out_per_in = out_per_in
+        self.kind = kind
+        self.M = M
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_free(self.h)
+            self.h = None
+
+    @property
+    def in_dt(self):
+        return _IN_DT[self.dtype]
+
+    def execute_block(self, x):
+        x = np.ascontiguousarray(x, dtype=self.in_dt)
+        cap = len(x) * self.out_per_in
+        out = np.zeros(max(cap, 1), dtype=self.in_dt)
+        n = lib().orc_execute_block(self.h, _ptr(x), len(x), _ptr(out))
+        return out[:n]
+
+    def push(self, s):
+        a = np.array([s], dtype=self.in_dt)
+        lib().orc_push(self.h, _ptr(a))
+
+    def write(self, xs):
+        a = np.ascontiguousarray(xs, dtype=self.in_dt)
+        lib().orc_write(self.h, _ptr(a), len(a))
+
+    def reset(self):
+        lib().orc_reset(self.h)
+
+    def group_delay(self, f):
+        return lib().orc_group_delay(self.h, f)
+
+    def frequency_response(self, f):
+        out = np.zeros(2)
+        lib().orc_frequency_response(self.h, f, _dptr(out))
+        return complex(out[0], out[1])
+
+    def pfb_execute(self, index):
+        out = np.zeros(1, dtype=self.in_dt)
+        rc = lib().orc_pfb_execute(self.h, self.dtype, index, _ptr(out))
+        if rc:
+            raise IndexError(index)
+        return out[0]
+
+
+def _mk(fn, *args):
+    err = C.c_int(0)
+    h = fn(*args, C.byref(err))
+    if not h:
+        raise ValueError(f"oracle construction error {err.value}")
+    return h
+
+
+def fir(dtype, taps, scale):
+    t = np.ascontiguousarray(taps, dtype=_COEF_DT[dtype])
+    s = np.array([scale], dtype=_COEF_DT[dtype])
+    return OracleObj(_mk(lib().orc_fir_new, dtype, _ptr(t), len(t), _ptr(s)), dtype)
+
+
+def decim(dtype, taps, scale, M):
+    t = np.ascontiguousarray(taps, dtype=_COEF_DT[dtype])
+    s = np.array([scale], dtype=_COEF_DT[dtype])
+    return OracleObj(_mk(lib().orc_decim_new, dtype, _ptr(t), len(t), _ptr(s), M), dtype, kind="decim", M=M)
+
+
+def pfb(dtype, taps, M, scale):
+    t = np.ascontiguousarray(taps, dtype=_COEF_DT[dtype])
+    s = np.array([scale], dtype=_COEF_DT[dtype])
+    return OracleObj(_mk(lib().orc_pfb_new, dtype, _ptr(t), len(t), M, _ptr(s)), dtype, out_per_in=M, kind="pfb", M=M)
+
+
+def interp(dtype, taps, M):
+    t = np.ascontiguousarray(taps, dtype=_COEF_DT[dtype])
+    return OracleObj(_mk(lib().orc_interp_new, dtype, _ptr(t), len(t), M), dtype, out_per_in=M, kind="interp", M=M)
+
+
+def iir(dtype, ff, fb, type_):
+    a = np.ascontiguousarray(ff, dtype=_COEF_DT[dtype])
+    b = np.ascontiguousarray(fb, dtype=_COEF_DT[dtype])
+    return OracleObj(_mk(lib().orc_iir_new, dtype, _ptr(a), len(a), _ptr(b), len(b), type_), dtype, kind="iir")
+
+
+def iir_decim(dtype, ff, fb, type_, M):
+    a = np.ascontiguousarray(ff, dtype=_COEF_DT[dtype])
+    b = np.ascontiguousarray(fb, dtype=_COEF_DT[dtype])
+    return OracleObj(_mk(lib().orc_iir_decim_new, dtype, _ptr(a), len(a), _ptr(b), len(b), type_, M), dtype,
+                     kind="iir_decim", M=M)
+
+
+def iir_interp(dtype, ff, fb, type_, M):
+    a = np.ascontiguousarray(ff, dtype=_COEF_DT[dtype])
+    b = np.ascontiguousarray(fb, dtype=_COEF_DT[dtype])
+    return OracleObj(_mk(lib().orc_iir_interp_new, dtype, _ptr(a), len(a), _ptr(b), len(b), type_, M), dtype,
+                     out_per_in=M, kind="iir_interp", M=M)
+
+
+def firdes_kaiser(n, fc, as_, mu):
+    h = np.zeros(n)
+    rc = lib().orc_firdes_kaiser(n, fc, as_, mu, _dptr(h))
+    if rc:
+        raise ValueError(rc)
+    return h
+
+
+def firdes_notch(m, f0, as_):
+    h = np.zeros(2 * m + 1)
+    rc = lib().orc_firdes_notch(m, f0, as_, _dptr(h))
+    if rc:
+        raise ValueError(rc)
+    return h
+
+
+def active_lag(bw, zeta, k):
+    n, d = np.zeros(3), np.zeros(3)
+    rc = lib().orc_active_lag(bw, zeta, k, _dptr(n), _dptr(d))
+    if rc:
+        raise ValueError(rc)
+    return n, d
+
+
+def synth(seed, channel, start, count, complex_=False):
+    """Build-defined synthetic stream.  count = samples."""
+    scal = count * (2 if complex_ else 1)
+    out = np.zeros(scal, dtype=np.float32)
+    lib().orc_synth_f32(seed, channel, start * (2 if complex_ else 1), scal,
+                        out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out.view(np.complex64) if complex_ else out

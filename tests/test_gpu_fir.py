@@ -1,0 +1,255 @@
+"""GPU parity tests for the FIR family (FIRFilter, DecimatingFIRFilter,
+PolyPhaseFilterBank, InterpolatingFIRFilter) against the CPU restatement
+(oracle/).  EXACT kernels must be bit-identical to the restatement at the
+same precision; FMA / FFT kernels within the §8d tolerance against the f64
+restatement:  rel_RMS <= 1e-6 and max|err| <= 1e-6 * sum|h| * max|x|."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from gpu_util import bits_equal, rel_rms, to_dev, empty_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+sd = pytest.importorskip("solid_dsp_amd")
+from solid_dsp_amd import FIRFilter, DecimatingFIRFilter, PolyPhaseFilterBank, InterpolatingFIRFilter  # noqa: E402
+
+C64, C128, F32, F64 = np.complex64, np.complex128, np.float32, np.float64
+DTYPES = [  # (sdsp dtype, coef dtype, sample dtype)
+    (O.RR32, F32, F32), (O.RC32, F32, C64), (O.CC32, C64, C64),
+    (O.RR64, F64, F64), (O.RC64, F64, C128), (O.CC64, C128, C128),
+]
+
+
+def rand(rng, n, dt):
+    if np.dtype(dt).kind == "c":
+        return (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(dt)
+    return rng.standard_normal(n).astype(dt)
+
+
+# ---------------------------------------------------------------- KATs
+def test_fir_kats_through_device():  # src/filter/fir/mod.rs:200-206, 226-232
+    f = FIRFilter(np.array([1.0, 2, 3, 4, 5]), 1.0, sample_dtype=C128)
+    assert f.execute(2.02 + 0j) == [complex(10.1, 0.0)]
+    f = FIRFilter(np.array([1.0, 2, 3, 4, 5]), 1.0, sample_dtype=C128)
+    y = f.execute_block(np.array([2.02, 4.04, 1.02, 0.23, 9.19], dtype=C128))
+    assert y[4] == complex(60.03, 0.0)
+
+
+def test_decim_kats_through_device():  # src/filter/fir/decim.rs:213-219, 242-248
+    d = DecimatingFIRFilter(np.array([1.0, 2, 3, 4, 5]), 1.0, 2, sample_dtype=C128)
+    assert d.execute(2.02 + 0j) == []
+    assert d.execute(4.04 + 0j) == [complex(28.28, 0.0)]
+    d = DecimatingFIRFilter(np.array([1.0, 2, 3, 4, 5]), 1.0, 2, sample_dtype=C128)
+    y = d.execute_block(np.array([2.02, 4.04, 1.02, 0.23], dtype=C128))
+    assert list(y) == [complex(28.28, 0.0), complex(21.39, 0.0)]
+
+
+def test_accessors_mirror_reference():
+    f = FIRFilter(np.arange(1.0, 6.0), 1.0, sample_dtype=C128)
+    f.set_scale(2.0)
+    assert f.get_scale() == 2.0  # fir/mod.rs:103-124
+    assert f.len() == 5 and not f.is_empty()
+    assert list(f.coefficients()) == [5.0, 4.0, 3.0, 2.0, 1.0]  # REVERSE storage
+    d = DecimatingFIRFilter(np.zeros(12), 1.0, 2, sample_dtype=C128)
+    assert d.get_decimation() == 2 and d.len() == 12
+
+
+def test_errors_mirror_reference():
+    with pytest.raises(sd.SdspError) as e:
+        FIRFilter(np.array([], dtype=F64), 1.0)
+    assert e.value.code == 1
+    with pytest.raises(sd.SdspError) as e:
+        DecimatingFIRFilter(np.ones(3), 1.0, 0)
+    assert e.value.code == 2
+    with pytest.raises(sd.SdspError) as e:
+        InterpolatingFIRFilter(np.ones(3), 0)
+    assert e.value.code == 3
+    with pytest.raises(sd.SdspError) as e:
+        PolyPhaseFilterBank(np.ones(3), 0, 1.0)
+    assert e.value.code == 4
+
+
+def test_freq_response_and_group_delay_match_oracle():  # fir/mod.rs:253-261, 284-291
+    h = O.firdes_notch(25, 0.35, 120.0)
+    f = FIRFilter(h, 1.0, sample_dtype=F64)
+    r = f.frequency_response(0.0)
+    assert round(r.real) == 1.0 and r.imag == 0.0
+    o = O.fir(O.RR64, h, 1.0)
+    for fr in (0.0, 0.1, -0.3, 0.5):
+        assert f.frequency_response(fr) == o.frequency_response(fr)
+        assert f.group_delay(fr) == o.group_delay(fr)
+    h12 = O.firdes_notch(12, 0.35, 120.0)
+    assert int(FIRFilter(h12, 1.0, sample_dtype=F64).group_delay(0.0) + 0.5) == 12
+
+
+# ---------------------------------------------------------------- exact FIR parity
+@pytest.mark.parametrize("dt,cdt,sdt", DTYPES)
+@pytest.mark.parametrize("L", [1, 5, 63, 256, 300, 777])
+def test_fir_exact_bit_parity(dt, cdt, sdt, L):
+    rng = np.random.default_rng(L * 7 + dt)
+    h = rand(rng, L, cdt)
+    scale = cdt(0.75) if np.dtype(cdt).kind == "f" else cdt(0.75 - 0.25j)
+    x = rand(rng, 5000, sdt)
+    f = FIRFilter(h, scale, sample_dtype=sdt, algo=sd.ALGO_EXACT)
+    o = O.fir(dt, h, scale)
+    # streaming across calls of ragged sizes, including empty and single-sample blocks
+    cuts = [0, 1, 1, 37, 37, 2048, 4999, 5000]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        y = f.execute_block(x[a:b])
+        yo = o.execute_block(x[a:b])
+        assert bits_equal(y, yo), (L, a, b)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", [DTYPES[1], DTYPES[2], DTYPES[4]])
+def test_fir_fma_tolerance(dt, cdt, sdt):
+    rng = np.random.default_rng(11)
+    h = rand(rng, 256, cdt)
+    x = rand(rng, 20000, sdt)
+    y = FIRFilter(h, 1.0, sample_dtype=sdt, algo=sd.ALGO_FMA).execute_block(x)
+    ref = O.fir(O.CC64, h.astype(C128), 1.0 + 0j).execute_block(x.astype(C128))
+    assert rel_rms(y, ref) <= 1e-6
+
+
+def _f32_taps(L, fc):
+    return O.firdes_kaiser(L, fc, 80.0, 0.0).astype(F32)
+
+
+@pytest.mark.parametrize("dt,cdt", [(O.RC32, F32), (O.CC32, C64)])
+@pytest.mark.parametrize("L", [2, 64, 256, 257, 1000])
+def test_fir_fft_tolerance(dt, cdt, L):
+    # overlap-save vs the f64 restatement on the same f32-representable operands (§8d)
+    h = _f32_taps(L, 0.1)
+    if cdt == C64:
+        h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
+    x = O.synth(20250226, 0, 0, 300000, complex_=True)
+    f = FIRFilter(h, cdt(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    y = np.concatenate([f.execute_block(x[:70001]), f.execute_block(x[70001:])])
+    ref = O.fir(O.CC64, h.astype(C128), 0.2 + 0j).execute_block(x.astype(C128))
+    assert rel_rms(y, ref) <= 1e-6
+    bound = 1e-6 * np.abs(h).sum() * 0.2 * np.abs(x).max()
+    assert np.abs(y - ref).max() <= bound
+
+
+def test_fir_fft_matches_exact_kernel_across_calls():
+    h = _f32_taps(256, 0.1)
+    x = O.synth(7, 3, 0, 200000, complex_=True)
+    a = FIRFilter(h, F32(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    b = FIRFilter(h, F32(0.2), sample_dtype=C64, algo=sd.ALGO_EXACT)
+    ya = np.concatenate([a.execute_block(x[i:i + 65537]) for i in range(0, len(x), 65537)])
+    yb = b.execute_block(x)
+    assert rel_rms(ya, yb) <= 1e-6
+
+
+def test_fir_state_clone_reset():
+    rng = np.random.default_rng(5)
+    h = rand(rng, 31, F64)
+    x = rand(rng, 400, C128)
+    f = FIRFilter(h, 1.0, sample_dtype=C128, algo=sd.ALGO_EXACT)
+    f.execute_block(x[:200])
+    g = f.clone()
+    assert bits_equal(f.execute_block(x[200:]), g.execute_block(x[200:]))
+    hist, ph = g.get_state()
+    assert bits_equal(hist, x[-30:])
+    f.reset()
+    assert bits_equal(f.execute_block(x[:50]), O.fir(O.RC64, h, 1.0).execute_block(x[:50]))
+
+
+def test_fir_multichannel_device_matches_single():
+    import torch
+    rng = np.random.default_rng(9)
+    h = _f32_taps(256, 0.1)
+    ch, n = 3, 100000
+    x = np.stack([O.synth(1, c, 0, n, complex_=True) for c in range(ch)])
+    f = FIRFilter(h, F32(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_EXACT)
+    d_in = to_dev(x.reshape(-1))
+    d_out = empty_dev(ch * n, C64)
+    f.execute_block_device(d_in, n, d_out, torch.cuda.current_stream())
+    y = to_host(d_out).reshape(ch, n)
+    for c in range(ch):
+        ref = O.fir(O.RC32, h, F32(0.2)).execute_block(x[c])
+        assert bits_equal(y[c], ref)
+
+
+# ---------------------------------------------------------------- decimator
+@pytest.mark.parametrize("dt,cdt,sdt", DTYPES)
+@pytest.mark.parametrize("L,M", [(5, 2), (256, 32), (300, 7), (16, 64), (1, 3)])
+def test_decim_exact_bit_parity(dt, cdt, sdt, L, M):
+    rng = np.random.default_rng(L + M + dt)
+    h = rand(rng, L, cdt)
+    x = rand(rng, 3000, sdt)
+    d = DecimatingFIRFilter(h, cdt(0.5), M, sample_dtype=sdt, algo=sd.ALGO_EXACT)
+    o = O.decim(dt, h, cdt(0.5), M)
+    for a, b in [(0, 1), (1, 2), (2, 35), (35, 35), (35, 1700), (1700, 3000)]:
+        y = d.execute_block(x[a:b])
+        yo = o.execute_block(x[a:b])
+        assert bits_equal(y, yo), (a, b)
+    d.push(x[0]); o.push(x[0])
+    d.write(x[:13]); o.write(x[:13])
+    assert bits_equal(d.execute_block(x[:500]), o.execute_block(x[:500]))
+
+
+def test_decim_cfg4_shape():
+    # cfg4: 32 branches x 8 taps, M = 32, crcf
+    h = O.firdes_kaiser(256, 1.0 / 64, 80.0, 0.0).astype(F32)
+    x = O.synth(20250226, 4, 0, 1 << 18, complex_=True)
+    d = DecimatingFIRFilter(h, F32(1.0 / 32), 32, sample_dtype=C64, algo=sd.ALGO_EXACT)
+    y = d.execute_block(x)
+    assert len(y) == (1 << 18) // 32
+    assert bits_equal(y, O.decim(O.RC32, h, F32(1.0 / 32), 32).execute_block(x))
+    ref = O.decim(O.RC64, h.astype(F64), 1.0 / 32, 32).execute_block(x.astype(C128))
+    assert rel_rms(y, ref) <= 1e-6
+
+
+# ---------------------------------------------------------------- PFB / interpolator
+@pytest.mark.parametrize("dt,cdt,sdt", DTYPES)
+@pytest.mark.parametrize("L,M", [(18, 4), (64, 8), (10, 4), (7, 7)])
+def test_pfb_exact_bit_parity(dt, cdt, sdt, L, M):
+    rng = np.random.default_rng(L * M + dt)
+    h = rand(rng, L, cdt)
+    x = rand(rng, 700, sdt)
+    p = PolyPhaseFilterBank(h, M, cdt(3.0), sample_dtype=sdt)
+    o = O.pfb(dt, h, M, cdt(3.0))
+    assert bits_equal(p.execute_block(x[:300]), o.execute_block(x[:300]))
+    assert bits_equal(p.execute_block(x[300:]), o.execute_block(x[300:]))
+    p.push(x[5]); o.push(x[5])
+    for idx in range(M):
+        assert bits_equal(np.array([p.execute(idx)]), np.array([o.pfb_execute(idx)]))
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", DTYPES)
+@pytest.mark.parametrize("L,M", [(10, 4), (64, 8), (9, 3), (5, 1)])
+def test_interp_exact_bit_parity(dt, cdt, sdt, L, M):
+    rng = np.random.default_rng(L * 31 + M + dt)
+    h = rand(rng, L, cdt)
+    x = rand(rng, 513, sdt)
+    f = InterpolatingFIRFilter(h, M, sample_dtype=sdt)
+    o = O.interp(dt, h, M)
+    assert bits_equal(f.execute_block(x[:200]), o.execute_block(x[:200]))
+    assert bits_equal(f.execute_block(x[200:]), o.execute_block(x[200:]))
+    if dt in (O.RR64, O.RC64):
+        for fr in (0.0, 0.05, 0.25):
+            assert f.frequency_response(fr) == o.frequency_response(fr)
+            assert f.group_delay(fr) == o.group_delay(fr)
+
+
+def test_pfb_reset():
+    rng = np.random.default_rng(3)
+    h = rand(rng, 32, F64)
+    x = rand(rng, 40, C128)
+    p = PolyPhaseFilterBank(h, 4, 1.0, sample_dtype=C128)
+    p.execute_block(x)
+    p.reset()
+    assert bits_equal(p.execute_block(x), O.pfb(O.RC64, h, 4, 1.0).execute_block(x))
+
+
+# ---------------------------------------------------------------- synthetic stream
+def test_device_synth_matches_host():
+    import torch
+    n = 1 << 20
+    d = torch.empty(n, dtype=torch.float32, device="cuda")
+    lib = sd.lib()
+    assert lib.sdsp_synth_f32_device(d.data_ptr(), 20250226, 5, 1000, n, None) == 0
+    got = to_host(d)
+    ref = O.synth(20250226, 5, 1000, n)
+    assert bits_equal(got, ref)
