@@ -22,7 +22,10 @@
  *    (the reference types are !Send); distinct handles may run concurrently.
  *  - `*_execute_block` takes HOST slices (like `&[In] -> Vec<Out>`) and is
  *    PCIe-bound; `*_execute_block_device` takes device pointers (HBM resident)
- *    and a hipStream_t (NULL = the handle's stream) and is asynchronous.
+ *    and a hipStream_t and is asynchronous.  NULL = the handle's own stream;
+ *    the legacy null stream is passed as hipStreamLegacy ((void*)1).  Calls on
+ *    one handle must be stream-ordered (the delay line is updated in HBM at
+ *    the end of every call).
  *  - No CPU fallback: with no usable gfx950 device every create call returns
  *    SDSP_E_NO_DEVICE.
  */
@@ -110,6 +113,17 @@ SDSP_API int sdsp_decim_create(sdsp_fir** out, int dtype, const void* taps, size
 SDSP_API int sdsp_fir_set_channels(sdsp_fir* h, size_t channels);
 SDSP_API int sdsp_fir_set_algo(sdsp_fir* h, int algo);
 SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
+/* kernel-variant knobs (performance only; results are identical across values, except
+ * SDSP_TUNE_OLS_ABLATE_NOMEM, a profiling ablation that skips HBM traffic and leaves the
+ * output unwritten) */
+typedef enum {
+    SDSP_TUNE_OLS_WIDE = 1,
+    SDSP_TUNE_OLS_INTERLEAVE = 2,
+    SDSP_TUNE_OLS_DEPTH2 = 3,
+    SDSP_TUNE_OLS_ABLATE_NOMEM = 4,
+    SDSP_TUNE_OLS_OCCUPANCY = 5 /* 0 = 2-wave kernel, 3/4 = single-region kernel at 3/4 blocks per CU */
+} sdsp_tune_key;
+SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */
 /* Clone (derive(Clone), fir/mod.rs:58): same taps and a snapshot of the delay line */
 SDSP_API int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out);
@@ -182,12 +196,65 @@ SDSP_API int sdsp_pfb_group_delay(const sdsp_pfb* h, double f, double* delay);
 SDSP_API int sdsp_pfb_synchronize(sdsp_pfb* h);
 
 /* ------------------------------------------------------------------------
+ * IIR family  (IIRFilter src/filter/iir/mod.rs:62-414, SecondOrderFilter
+ *  src/filter/iir/sos.rs:34-231, DecimatingIIRFilter src/filter/iir/decim.rs:5-280,
+ *  InterpolatingIIRFilter src/filter/iir/interp.rs:6-268).
+ * dtype: SDSP_RR32, SDSP_RC32, SDSP_RR64, SDSP_RC64 (real coefficients, like
+ * the reference's Conj + Real bound).  type: 0 = Normal, 1 = SecondOrder.
+ * algo: SDSP_ALGO_EXACT = reference-order serial recurrence (one lane per
+ * channel, bit-identical); SDSP_ALGO_FMA = block-parallel scan (stable SOS
+ * cascades); SDSP_ALGO_AUTO = scan for long blocks when the cascade admits it.
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_iir sdsp_iir;
+
+/* IIRFilter::new(&ff, &fb, IIRFilterType)            mod.rs:92-164 */
+SDSP_API int sdsp_iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void* fb, size_t nfb,
+                             int type, int device);
+/* DecimatingIIRFilter::new(&ff, &fb, type, M)         decim.rs:11-30 */
+SDSP_API int sdsp_iir_decim_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void* fb,
+                                   size_t nfb, int type, size_t decimation, int device);
+/* InterpolatingIIRFilter::new(&ff, &fb, type, M)      interp.rs:12-31 */
+SDSP_API int sdsp_iir_interp_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void* fb,
+                                    size_t nfb, int type, size_t interpolation, int device);
+/* SecondOrderFilter::new(&ff, &fb) (f64)              sos.rs:55-75 */
+SDSP_API int sdsp_sos_create(sdsp_iir** out, const double* ff, size_t nff, const double* fb, size_t nfb,
+                             int device);
+SDSP_API void sdsp_iir_destroy(sdsp_iir* h);
+SDSP_API int sdsp_iir_clone(const sdsp_iir* h, sdsp_iir** out);
+SDSP_API int sdsp_iir_set_channels(sdsp_iir* h, size_t channels);
+SDSP_API int sdsp_iir_set_algo(sdsp_iir* h, int algo);
+/* scan plan of section group g: warm-up chunks (0 = scan not admissible) and chunk length */
+SDSP_API int sdsp_iir_scan_info(const sdsp_iir* h, int group, int* warmup_chunks, int* chunk);
+SDSP_API size_t sdsp_iir_output_count(const sdsp_iir* h, size_t n);
+/* Filter::execute / execute_block                     mod.rs:270-316, decim.rs:203-225, interp.rs:197-214 */
+SDSP_API int sdsp_iir_execute(sdsp_iir* h, const void* sample, void* out, size_t* n_out);
+SDSP_API int sdsp_iir_execute_block(sdsp_iir* h, const void* in, size_t n, void* out, size_t* n_out);
+SDSP_API int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void* d_out, size_t* n_out,
+                                           void* stream);
+SDSP_API int sdsp_iir_reset(sdsp_iir* h);
+/* state: SOS (w1, w2) per section per channel; Normal the last cap-1 w values, newest first */
+SDSP_API size_t sdsp_iir_state_len(const sdsp_iir* h);
+SDSP_API int sdsp_iir_get_state(const sdsp_iir* h, void* state, size_t* phase);
+SDSP_API int sdsp_iir_set_state(sdsp_iir* h, const void* state, size_t phase);
+/* numerator_coefs() / denominator_coefs() as stored (mod.rs:123-127,156-157); which: 0 num, 1 den */
+SDSP_API size_t sdsp_iir_num_coefs(const sdsp_iir* h, int which);
+SDSP_API int sdsp_iir_coefficients(const sdsp_iir* h, double* num, double* den);
+/* SecondOrderFilter numerator_coefs (a[1..]/a0) and denominator_coefs (b/a0) of one section */
+SDSP_API int sdsp_sos_section_coefs(const sdsp_iir* h, int section, double* num2, double* den3);
+/* Filter::frequency_response / group_delay (host f64)  mod.rs:336-413 */
+SDSP_API int sdsp_iir_frequency_response(const sdsp_iir* h, double f, double* re_im);
+SDSP_API int sdsp_iir_group_delay(const sdsp_iir* h, double f, double* delay);
+SDSP_API int sdsp_iir_synchronize(sdsp_iir* h);
+
+/* ------------------------------------------------------------------------
  * Device utilities
  * ------------------------------------------------------------------------ */
 /* Synthetic stream (build-defined): `count` f32 scalars
  * x(i) = ((mix64(seed ^ channel*G + (start+i+1)*G) >> 40) * 2^-24) * 2 - 1 */
 SDSP_API int sdsp_synth_f32_device(void* d_out, uint64_t seed, uint64_t channel, uint64_t start,
                                    size_t count, void* stream);
+/* STREAM-style 16-B-per-lane device copy (HBM bandwidth calibration) */
+SDSP_API int sdsp_bandwidth_copy_device(const void* d_src, void* d_dst, size_t bytes, void* stream);
 /* Host-side reference FIR tap design (src/filter/firdes/mod.rs:278-305) */
 SDSP_API int sdsp_firdes_kaiser(size_t n, double fc, double as, double mu, double* h);
 SDSP_API int sdsp_firdes_notch(size_t m, double f0, double as, double* h);

@@ -10,7 +10,8 @@ from ._lib import (SdspError, lib, LIB_PATH, RR32, RC32, CC32, RR64, RC64, CC64,
                    ALGO_AUTO, ALGO_EXACT, ALGO_FMA, ALGO_FFT)
 from . import filter, group_delay  # noqa: F401
 from .filter import (Filter, FIRFilter, DecimatingFIRFilter, PolyPhaseFilterBank,  # noqa: F401
-                     InterpolatingFIRFilter)
+                     InterpolatingFIRFilter, IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter,
+                     InterpolatingIIRFilter)
 
 __version__ = "0.1.0"
 

@@ -76,6 +76,7 @@ def _declare(L):
         "sdsp_fir_set_channels": (i, [vp, sz]),
         "sdsp_fir_set_algo": (i, [vp, i]),
         "sdsp_fir_get_algo": (i, [vp]),
+        "sdsp_fir_set_tuning": (i, [vp, i, i]),
         "sdsp_fir_destroy": (None, [vp]),
         "sdsp_fir_clone": (i, [vp, vpp]),
         "sdsp_fir_set_scale": (i, [vp, vp]),
@@ -114,6 +115,7 @@ def _declare(L):
         "sdsp_pfb_group_delay": (i, [vp, d, dp]),
         "sdsp_pfb_synchronize": (i, [vp]),
         "sdsp_synth_f32_device": (i, [vp, C.c_uint64, C.c_uint64, C.c_uint64, sz, vp]),
+        "sdsp_bandwidth_copy_device": (i, [vp, vp, sz, vp]),
         "sdsp_firdes_kaiser": (i, [sz, d, d, d, dp]),
         "sdsp_firdes_notch": (i, [sz, d, d, dp]),
         "sdsp_kaiser_beta": (d, [d]),
@@ -157,6 +159,8 @@ def _optional_sigs():
         "sdsp_iir_coefficients": (i, [vp, dp, dp]),
         "sdsp_iir_num_coefs": (sz, [vp, i]),
         "sdsp_iir_synchronize": (i, [vp]),
+        "sdsp_iir_scan_info": (i, [vp, i, C.POINTER(i), C.POINTER(i)]),
+        "sdsp_sos_section_coefs": (i, [vp, i, dp, dp]),
         "sdsp_sos_create": (i, [vpp, C.POINTER(C.c_double), sz, C.POINTER(C.c_double), sz, i]),
         "sdsp_chan_create": (i, [vpp, vp, sz, sz, i]),
         "sdsp_chan_destroy": (None, [vp]),
@@ -216,9 +220,14 @@ def device_ptr(t) -> int:
     return int(t.data_ptr())
 
 
+HIP_STREAM_LEGACY = 1  # hipStreamLegacy: the legacy null stream (torch's default stream)
+
+
 def stream_handle(stream) -> int | None:
+    """None -> the handle's own stream; a torch stream (or raw handle) -> that
+    stream, with handle 0 (torch's default stream) mapped to hipStreamLegacy
+    because NULL means "the handle's stream" in the C ABI."""
     if stream is None:
         return None
-    if isinstance(stream, int):
-        return stream
-    return int(stream.cuda_stream)
+    h = stream if isinstance(stream, int) else int(stream.cuda_stream)
+    return h if h != 0 else HIP_STREAM_LEGACY

@@ -97,6 +97,8 @@ struct sdsp_fir {
     DevBuf stage_in, stage_out;
     // overlap-save plan
     bool ols_ok = false;
+    bool ols_wide = false, ols_interleave = true, ols_depth2 = false, ols_nomem = false;
+    int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
     OlsPlan ols{};
     DevBuf d_H, d_tw1, d_tw2;
 };
@@ -170,7 +172,7 @@ int ols_build(sdsp_fir* h) {
     SDSP_TRY(hipMemcpyAsync(h->d_tw1.p, tw1.data(), tw1.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw1");
     SDSP_TRY(hipMemcpyAsync(h->d_tw2.p, tw2.data(), tw2.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw2");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
-    h->ols = OlsPlan{h->d_H.p, h->d_tw1.p, h->d_tw2.p, h2};
+    h->ols = OlsPlan{h->d_H.p, h->d_tw1.p, h->d_tw2.p, h2, h->ols_wide, h->ols_interleave, h->ols_depth2, h->ols_nomem, h->ols_occ};
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -301,6 +303,24 @@ int sdsp_fir_set_algo(sdsp_fir* h, int algo) {
 }
 
 int sdsp_fir_get_algo(const sdsp_fir* h) { return h ? h->algo : -1; }
+
+int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    switch (key) {
+        case SDSP_TUNE_OLS_WIDE: h->ols_wide = value != 0; break;
+        case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
+        case SDSP_TUNE_OLS_DEPTH2: h->ols_depth2 = value != 0; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = value != 0; break;
+        case SDSP_TUNE_OLS_OCCUPANCY: h->ols_occ = (value == 3 || value == 4) ? value : 0; break;
+        default: return SDSP_E_INVALID_ARGUMENT;
+    }
+    h->ols.wide = h->ols_wide;
+    h->ols.interleave = h->ols_interleave;
+    h->ols.depth2 = h->ols_depth2;
+    h->ols.nomem = h->ols_nomem;
+    h->ols.occ = h->ols_occ;
+    return SDSP_OK;
+}
 
 int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out) {
     if (!h || !out) return SDSP_E_INVALID_ARGUMENT;
@@ -766,6 +786,15 @@ int sdsp_pfb_synchronize(sdsp_pfb* h) {
 // ===========================================================================
 // utilities
 // ===========================================================================
+int sdsp_bandwidth_copy_device(const void* d_src, void* d_dst, size_t bytes, void* stream) {
+    int dev = 0;
+    SDSP_TRY(hipGetDevice(&dev), "get device");
+    hipDeviceProp_t p;
+    SDSP_TRY(hipGetDeviceProperties(&p, dev), "props");
+    SDSP_TRY(launch_bw_copy(d_src, d_dst, bytes, p.multiProcessorCount, (hipStream_t)stream), "bw copy");
+    return SDSP_OK;
+}
+
 int sdsp_synth_f32_device(void* d_out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,
                           void* stream) {
     SDSP_TRY(launch_synth_f32((float*)d_out, seed, channel, start, count, (hipStream_t)stream), "synth");

@@ -1,0 +1,574 @@
+// C-ABI runtime for the IIR family: IIRFilter (Normal / SecondOrder),
+// SecondOrderFilter, DecimatingIIRFilter, InterpolatingIIRFilter
+// (src/filter/iir/{mod,sos,decim,interp}.rs).  Coefficient normalisation by
+// a0 happens here, once, in the handle's Coef precision exactly as the
+// reference does it (sos.rs:61-68, mod.rs:111-118); the streaming recurrence
+// runs in kern_iir.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sdsp.h"
+#include "sdsp_host.hpp"
+#include "sdsp_kernels.hpp"
+
+using namespace sdsp;
+
+namespace {
+
+#define IIR_TRY(expr, what)                                    \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return device_status(_e, what);  \
+    } while (0)
+
+constexpr int kMaxGroupSections = 8;  // sections per kernel launch (longer cascades chain launches)
+constexpr int kScanLanes = 256;
+constexpr int kMaxNormalCap = 32;
+
+struct Group {
+    int first = 0, count = 0;  // sections [first, first+count)
+    int wc = 0;                // warm-up chunks for the scan path (0: scan not applicable)
+    DevBuf d_P;                // [8][2c][2c]
+};
+
+struct DeviceGuardI {
+    int prev = -1;
+    explicit DeviceGuardI(int d) {
+        (void)hipGetDevice(&prev);
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~DeviceGuardI() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+using Mat = std::vector<double>;  // row-major D x D
+Mat matmul(const Mat& a, const Mat& b, int D) {
+    Mat c(D * D, 0.0);
+    for (int i = 0; i < D; ++i)
+        for (int k = 0; k < D; ++k) {
+            const double v = a[i * D + k];
+            if (v == 0.0) continue;
+            for (int j = 0; j < D; ++j) c[i * D + j] += v * b[k * D + j];
+        }
+    return c;
+}
+Mat matpow(Mat a, long long e, int D) {
+    Mat r(D * D, 0.0);
+    for (int i = 0; i < D; ++i) r[i * D + i] = 1.0;
+    while (e > 0) {
+        if (e & 1) r = matmul(r, a, D);
+        a = matmul(a, a, D);
+        e >>= 1;
+    }
+    return r;
+}
+double norm_inf(const Mat& a, int D) {
+    double m = 0.0;
+    for (int i = 0; i < D; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < D; ++j) s += std::fabs(a[i * D + j]);
+        m = std::max(m, s);
+    }
+    return m;
+}
+
+}  // namespace
+
+struct sdsp_iir {
+    int dtype = 0, device = 0, cus = 256;
+    int type = 1;       // 0 Normal, 1 SecondOrder
+    int mode = 0;       // 0 IIRFilter, 1 DecimatingIIRFilter, 2 InterpolatingIIRFilter
+    size_t M = 1;
+    size_t channels = 1;
+    size_t phase = 0;   // DecimatingIIRFilter::index (decim.rs:9)
+    std::vector<unsigned char> ff, fb;   // as given (Coef type)
+    std::vector<double> c64;             // normalised coefficients widened (host queries)
+    std::vector<unsigned char> cdev;     // normalised coefficients in the Coef type (device layout)
+    int S = 0, nb = 0, na = 0, cap = 0;
+    std::vector<Group> groups;
+    DevBuf d_coefs, d_state[2], d_tmp[2];
+    int cur = 0;
+    int algo = SDSP_ALGO_AUTO;
+    hipStream_t stream = nullptr;
+    DevBuf stage_in, stage_out;
+    size_t state_per_ch() const { return type == 1 ? (size_t)(2 * S) : (size_t)(cap - 1); }
+};
+
+namespace {
+
+bool is_f32(int dt) { return dt == SDSP_RR32 || dt == SDSP_RC32; }
+
+// one Coef value from raw bytes
+double cval(const std::vector<unsigned char>& v, int dt, size_t i) {
+    if (is_f32(dt)) { float f; std::memcpy(&f, v.data() + 4 * i, 4); return f; }
+    double d; std::memcpy(&d, v.data() + 8 * i, 8); return d;
+}
+// normalised value computed in the Coef type: num / den
+double cdiv_t(double num, double den, int dt) {
+    if (is_f32(dt)) return (double)((float)num / (float)den);
+    return num / den;
+}
+void push_coef(std::vector<unsigned char>& out, double v, int dt) {
+    if (is_f32(dt)) { float f = (float)v; const unsigned char* p = (const unsigned char*)&f; out.insert(out.end(), p, p + 4); }
+    else { const unsigned char* p = (const unsigned char*)&v; out.insert(out.end(), p, p + 8); }
+}
+
+int iir_alloc_state(sdsp_iir* h) {
+    const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
+    for (int i = 0; i < 2; ++i) {
+        IIR_TRY(h->d_state[i].ensure(sb), "alloc state");
+        if (sb) IIR_TRY(hipMemsetAsync(h->d_state[i].p, 0, sb, h->stream), "zero state");
+    }
+    h->cur = 0;
+    h->phase = 0;
+    IIR_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+// state-transition matrix of sections [first, first+count) with x = 0
+Mat sos_A(const sdsp_iir* h, int first, int count) {
+    const int D = 2 * count;
+    Mat A(D * D, 0.0);
+    for (int j = 0; j < D; ++j) {
+        std::vector<double> w1(count), w2(count);
+        for (int q = 0; q < count; ++q) { w1[q] = (2 * q == j) ? 1.0 : 0.0; w2[q] = (2 * q + 1 == j) ? 1.0 : 0.0; }
+        double v = 0.0;
+        for (int q = 0; q < count; ++q) {
+            const double* c = &h->c64[5 * (first + q)];
+            const double d = c[3] * w1[q] + c[4] * w2[q];
+            const double w = v - d;
+            v = c[0] * w + c[1] * w1[q] + c[2] * w2[q];
+            w2[q] = w1[q];
+            w1[q] = w;
+        }
+        for (int q = 0; q < count; ++q) {
+            A[(2 * q) * D + j] = w1[q];
+            A[(2 * q + 1) * D + j] = w2[q];
+        }
+    }
+    return A;
+}
+
+int plan_groups(sdsp_iir* h) {
+    h->groups.clear();
+    if (h->type != 1) return SDSP_OK;
+    const int B = iir_scan_chunk(h->dtype);
+    const double tol = is_f32(h->dtype) ? 1e-9 : 1e-17;
+    for (int f = 0; f < h->S; f += kMaxGroupSections) {
+        h->groups.emplace_back();
+        Group& g = h->groups.back();
+        g.first = f;
+        g.count = std::min(kMaxGroupSections, h->S - f);
+        const int D = 2 * g.count;
+        const Mat A = sos_A(h, g.first, g.count);
+        const Mat AB = matpow(A, B, D);
+        // warm-up: smallest m with ||A^(mB)||_inf < tol, m <= lanes/2
+        Mat Am = AB;
+        g.wc = 0;
+        for (int m = 1; m <= kScanLanes / 2; ++m) {
+            const double nrm = norm_inf(Am, D);
+            if (!std::isfinite(nrm)) break;
+            if (nrm < tol) { g.wc = m; break; }
+            Am = matmul(Am, AB, D);
+        }
+        if (g.wc == 0) continue;
+        std::vector<unsigned char> P;
+        Mat Pk = AB;
+        for (int k = 0; k < 8; ++k) {
+            for (double v : Pk) push_coef(P, v, h->dtype);
+            Pk = matmul(Pk, Pk, D);
+        }
+        IIR_TRY(g.d_P.ensure(P.size()), "alloc P");
+        IIR_TRY(hipMemcpy(g.d_P.p, P.data(), P.size(), hipMemcpyHostToDevice), "copy P");
+    }
+    return SDSP_OK;
+}
+
+int iir_check(size_t nff, size_t nfb, int type) {
+    if (type == 0) {  // IIRFilter::new Normal (mod.rs:99-104)
+        if (nff == 0) { set_error("IIR Filter Error NumeratorLengthZero"); return SDSP_E_NUMERATOR_LENGTH_ZERO; }
+        if (nfb == 0) { set_error("IIR Filter Error DenominatorLengthZero"); return SDSP_E_DENOMINATOR_LENGTH_ZERO; }
+        return SDSP_OK;
+    }
+    if (type != 1) { set_error("bad IIR type"); return SDSP_E_INVALID_ARGUMENT; }
+    // SecondOrder (mod.rs:131-142)
+    if (nff != nfb) { set_error("IIR Filter Error SecondOrderSectionSizeMismatch"); return SDSP_E_SOS_SIZE_MISMATCH; }
+    if (nff == 0) { set_error("IIR Filter Error SecondOrderSectionSizeZero"); return SDSP_E_SOS_SIZE_ZERO; }
+    if (nff % 3 != 0) {
+        set_error("IIR Filter Error SecondOrderSectionSizeNotMultpleOf3");
+        return SDSP_E_SOS_SIZE_NOT_MULTIPLE_OF_3;
+    }
+    return SDSP_OK;
+}
+
+int iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void* fb, size_t nfb, int type, int mode,
+               size_t M, int device) {
+    *out = nullptr;
+    if (!(dtype == SDSP_RR32 || dtype == SDSP_RC32 || dtype == SDSP_RR64 || dtype == SDSP_RC64)) {
+        set_error("IIR filters take real coefficients (the reference implements Conj/Real for f64 only)");
+        return SDSP_E_UNSUPPORTED;
+    }
+    if (mode != 0) {  // decim.rs:191-200, interp.rs:185-194: empty checks, then the factor
+        if (nff == 0) { set_error("IIR Filter Error NumeratorLengthZero"); return SDSP_E_NUMERATOR_LENGTH_ZERO; }
+        if (nfb == 0) { set_error("IIR Filter Error DenominatorLengthZero"); return SDSP_E_DENOMINATOR_LENGTH_ZERO; }
+        if (M < 1) {
+            set_error(mode == 1 ? "IIR Filter Error DecimationLessThanOne" : "IIR Filter Error InterpolationLessThanOne");
+            return mode == 1 ? SDSP_E_IIR_DECIMATION_LESS_THAN_ONE : SDSP_E_IIR_INTERPOLATION_LESS_THAN_ONE;
+        }
+    }
+    int st = iir_check(nff, nfb, type);
+    if (st) return st;
+    const size_t cb = coef_bytes(dtype);
+    sdsp_iir* h = new sdsp_iir();
+    h->dtype = dtype;
+    h->device = device;
+    h->type = type;
+    h->mode = mode;
+    h->M = mode ? M : 1;
+    h->ff.assign((const unsigned char*)ff, (const unsigned char*)ff + nff * cb);
+    h->fb.assign((const unsigned char*)fb, (const unsigned char*)fb + nfb * cb);
+    if (type == 1) {
+        h->S = (int)(nff / 3);
+        for (int s = 0; s < h->S; ++s) {  // sos.rs:61-68: b = ff/a0, a = fb/a0 in the Coef type
+            const double a0 = cval(h->fb, dtype, 3 * s);
+            const double v[5] = {cdiv_t(cval(h->ff, dtype, 3 * s), a0, dtype), cdiv_t(cval(h->ff, dtype, 3 * s + 1), a0, dtype),
+                                 cdiv_t(cval(h->ff, dtype, 3 * s + 2), a0, dtype), cdiv_t(cval(h->fb, dtype, 3 * s + 1), a0, dtype),
+                                 cdiv_t(cval(h->fb, dtype, 3 * s + 2), a0, dtype)};
+            for (double x : v) { h->c64.push_back(x); push_coef(h->cdev, x, dtype); }
+        }
+    } else {
+        h->nb = (int)nff;
+        h->na = (int)nfb;
+        h->cap = (int)std::max(nff, nfb);  // mod.rs:105-109
+        if (h->cap > kMaxNormalCap) {
+            delete h;
+            set_error("Normal IIR order above 31 is not supported on the device");
+            return SDSP_E_UNSUPPORTED;
+        }
+        const double a0 = cval(h->fb, dtype, 0);
+        for (size_t i = 0; i < nff; ++i) { const double v = cdiv_t(cval(h->ff, dtype, i), a0, dtype); h->c64.push_back(v); push_coef(h->cdev, v, dtype); }
+        for (size_t i = 1; i < nfb; ++i) { const double v = cdiv_t(cval(h->fb, dtype, i), a0, dtype); h->c64.push_back(v); push_coef(h->cdev, v, dtype); }
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) {
+        delete h;
+        set_error("no HIP device visible (libsdsp has no CPU execution path)");
+        return SDSP_E_NO_DEVICE;
+    }
+    DeviceGuardI g(device);
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess || std::strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+        delete h;
+        set_error("libsdsp is built for gfx950");
+        return SDSP_E_NO_DEVICE;
+    }
+    h->cus = p.multiProcessorCount;
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = h->d_coefs.ensure(h->cdev.size());
+    if (e == hipSuccess) e = hipMemcpy(h->d_coefs.p, h->cdev.data(), h->cdev.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        st = device_status(e, "iir create");
+        sdsp_iir_destroy(h);
+        return st;
+    }
+    st = plan_groups(h);
+    if (!st) st = iir_alloc_state(h);
+    if (st) {
+        sdsp_iir_destroy(h);
+        return st;
+    }
+    *out = h;
+    return SDSP_OK;
+}
+
+bool group_scan(const sdsp_iir* h, const Group& g, size_t nd) {
+    if (h->type != 1 || g.wc == 0) return false;
+    if (h->algo == SDSP_ALGO_EXACT) return false;
+    if (h->algo == SDSP_ALGO_AUTO && nd < 8192) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdsp_iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void* fb, size_t nfb, int type,
+                    int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    return iir_create(out, dtype, ff, nff, fb, nfb, type, 0, 1, device);
+}
+int sdsp_iir_decim_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void* fb, size_t nfb, int type,
+                          size_t M, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    return iir_create(out, dtype, ff, nff, fb, nfb, type, 1, M, device);
+}
+int sdsp_iir_interp_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void* fb, size_t nfb,
+                           int type, size_t M, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    return iir_create(out, dtype, ff, nff, fb, nfb, type, 2, M, device);
+}
+int sdsp_sos_create(sdsp_iir** out, const double* ff, size_t nff, const double* fb, size_t nfb, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (nff < 3 || nfb < 3) {  // sos.rs:56-60
+        set_error("Second Order Error CoefficientsNotInRange");
+        return SDSP_E_SOS_COEFFICIENTS_NOT_IN_RANGE;
+    }
+    return iir_create(out, SDSP_RR64, ff, 3, fb, 3, 1, 0, 1, device);
+}
+
+void sdsp_iir_destroy(sdsp_iir* h) {
+    if (!h) return;
+    {
+        DeviceGuardI g(h->device);
+        if (h->stream) {
+            (void)hipStreamSynchronize(h->stream);
+            (void)hipStreamDestroy(h->stream);
+        }
+        h->d_coefs.release();
+        for (int i = 0; i < 2; ++i) { h->d_state[i].release(); h->d_tmp[i].release(); }
+        for (auto& g : h->groups) g.d_P.release();
+        h->stage_in.release();
+        h->stage_out.release();
+    }
+    delete h;
+}
+
+int sdsp_iir_clone(const sdsp_iir* h, sdsp_iir** out) {
+    if (!h || !out) return SDSP_E_INVALID_ARGUMENT;
+    const size_t cb = coef_bytes(h->dtype);
+    int st = iir_create(out, h->dtype, h->ff.data(), h->ff.size() / cb, h->fb.data(), h->fb.size() / cb, h->type,
+                        h->mode, h->M, h->device);
+    if (st) return st;
+    sdsp_iir* c = *out;
+    DeviceGuardI g(h->device);
+    c->algo = h->algo;
+    if (h->channels != 1) {
+        st = sdsp_iir_set_channels(c, h->channels);
+        if (st) return st;
+    }
+    IIR_TRY(hipStreamSynchronize(h->stream), "sync");
+    const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
+    if (sb) IIR_TRY(hipMemcpy(c->d_state[0].p, h->d_state[h->cur].p, sb, hipMemcpyDeviceToDevice), "clone state");
+    c->cur = 0;
+    c->phase = h->phase;
+    return SDSP_OK;
+}
+
+int sdsp_iir_set_channels(sdsp_iir* h, size_t channels) {
+    if (!h || channels == 0) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuardI g(h->device);
+    h->channels = channels;
+    return iir_alloc_state(h);
+}
+
+int sdsp_iir_set_algo(sdsp_iir* h, int algo) {
+    if (!h || !(algo == SDSP_ALGO_AUTO || algo == SDSP_ALGO_EXACT || algo == SDSP_ALGO_FMA)) return SDSP_E_INVALID_ARGUMENT;
+    h->algo = algo;  // FMA = always the block-parallel scan where the cascade admits it
+    return SDSP_OK;
+}
+
+int sdsp_iir_scan_info(const sdsp_iir* h, int group, int* warmup_chunks, int* chunk) {
+    if (!h || group < 0 || group >= (int)h->groups.size()) return SDSP_E_INVALID_ARGUMENT;
+    if (warmup_chunks) *warmup_chunks = h->groups[group].wc;
+    if (chunk) *chunk = iir_scan_chunk(h->dtype);
+    return SDSP_OK;
+}
+
+size_t sdsp_iir_output_count(const sdsp_iir* h, size_t n) {
+    if (!h) return 0;
+    if (h->mode == 2) return n * h->M;
+    if (h->mode == 1) {
+        const size_t j0 = (h->M - 1 - h->phase) % h->M;
+        return j0 < n ? (n - 1 - j0) / h->M + 1 : 0;
+    }
+    return n;
+}
+
+int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void* d_out, size_t* n_out, void* stream) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuardI g(h->device);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const size_t nout = sdsp_iir_output_count(h, n);
+    if (n_out) *n_out = nout;
+    if (n == 0) return SDSP_OK;
+    const int Mi = h->mode == 2 ? (int)h->M : 1;
+    const int Md = h->mode == 1 ? (int)h->M : 1;
+    const size_t nd = n * Mi;
+    const size_t sbytes = sample_bytes(h->dtype);
+    unsigned char* st_in = (unsigned char*)h->d_state[h->cur].p;
+    unsigned char* st_out = (unsigned char*)h->d_state[h->cur ^ 1].p;
+    const size_t cb = coef_bytes(h->dtype);
+    if (h->type == 0) {
+        IirArgs a{d_in, d_out, h->d_coefs.p, nullptr, st_in, st_out, n, nout, h->channels, 0, h->nb, h->na, h->cap,
+                  Mi, Md, h->phase, false, 0};
+        IIR_TRY(launch_iir(h->dtype, a, s), "iir normal");
+    } else {
+        const size_t ng = h->groups.size();
+        if (ng > 1) {
+            IIR_TRY(h->d_tmp[0].ensure(nd * h->channels * sbytes), "iir tmp");
+            IIR_TRY(h->d_tmp[1].ensure(nd * h->channels * sbytes), "iir tmp");
+        }
+        size_t soff = 0;
+        const void* src = d_in;
+        for (size_t gi = 0; gi < ng; ++gi) {
+            const Group& gr = h->groups[gi];
+            const bool first = gi == 0, last = gi + 1 == ng;
+            void* dst = last ? d_out : h->d_tmp[gi & 1].p;
+            const size_t n_g = first ? n : nd;
+            IirArgs a{src, dst, (const unsigned char*)h->d_coefs.p + 5 * gr.first * cb, gr.d_P.p,
+                      st_in + soff, st_out + soff, n_g, last ? nout : nd, h->channels, gr.count, 0, 0, 0,
+                      first ? Mi : 1, last ? Md : 1, last ? h->phase : 0, group_scan(h, gr, nd), gr.wc};
+            IIR_TRY(launch_iir(h->dtype, a, s), "iir sos");
+            soff += h->channels * 2 * gr.count * sbytes;
+            src = dst;
+        }
+    }
+    h->cur ^= 1;
+    if (h->mode == 1) h->phase = (h->phase + nd) % h->M;
+    return SDSP_OK;
+}
+
+int sdsp_iir_execute_block(sdsp_iir* h, const void* in, size_t n, void* out, size_t* n_out) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuardI g(h->device);
+    const size_t sb = sample_bytes(h->dtype);
+    const size_t nout = sdsp_iir_output_count(h, n);
+    if (n_out) *n_out = nout;
+    if (n == 0) return SDSP_OK;
+    IIR_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
+    IIR_TRY(h->stage_out.ensure(h->channels * std::max<size_t>(nout, 1) * sb), "stage out");
+    IIR_TRY(hipMemcpyAsync(h->stage_in.p, in, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
+    int st = sdsp_iir_execute_block_device(h, h->stage_in.p, n, h->stage_out.p, nullptr, h->stream);
+    if (st) return st;
+    if (nout) IIR_TRY(hipMemcpyAsync(out, h->stage_out.p, h->channels * nout * sb, hipMemcpyDeviceToHost, h->stream), "D2H");
+    IIR_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_iir_execute(sdsp_iir* h, const void* sample, void* out, size_t* n_out) {
+    if (!h || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
+    return sdsp_iir_execute_block(h, sample, 1, out, n_out);
+}
+
+int sdsp_iir_reset(sdsp_iir* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuardI g(h->device);
+    return iir_alloc_state(h);
+}
+
+size_t sdsp_iir_state_len(const sdsp_iir* h) { return h ? h->channels * h->state_per_ch() : 0; }
+
+int sdsp_iir_get_state(const sdsp_iir* h, void* state, size_t* phase) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuardI g(h->device);
+    IIR_TRY(hipStreamSynchronize(h->stream), "sync");
+    const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
+    if (state && sb) IIR_TRY(hipMemcpy(state, h->d_state[h->cur].p, sb, hipMemcpyDeviceToHost), "get state");
+    if (phase) *phase = h->phase;
+    return SDSP_OK;
+}
+
+int sdsp_iir_set_state(sdsp_iir* h, const void* state, size_t phase) {
+    if (!h || phase >= h->M) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuardI g(h->device);
+    IIR_TRY(hipStreamSynchronize(h->stream), "sync");
+    const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
+    if (state && sb) IIR_TRY(hipMemcpy(h->d_state[h->cur].p, state, sb, hipMemcpyHostToDevice), "set state");
+    h->phase = phase;
+    return SDSP_OK;
+}
+
+// numerator_coefs() / denominator_coefs() exactly as the reference stores them
+// (mod.rs:123-127 Normal: b/a0 and a[1..]/a0; :156-157 SecondOrder: raw ff and fb)
+size_t sdsp_iir_num_coefs(const sdsp_iir* h, int which) {
+    if (!h) return 0;
+    const size_t cb = coef_bytes(h->dtype);
+    if (h->type == 1) return (which == 0 ? h->ff.size() : h->fb.size()) / cb;
+    return which == 0 ? (size_t)h->nb : (size_t)(h->na - 1);
+}
+int sdsp_iir_coefficients(const sdsp_iir* h, double* num, double* den) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    const size_t nn = sdsp_iir_num_coefs(h, 0), nd = sdsp_iir_num_coefs(h, 1);
+    if (h->type == 1) {
+        for (size_t i = 0; i < nn; ++i) if (num) num[i] = cval(h->ff, h->dtype, i);
+        for (size_t i = 0; i < nd; ++i) if (den) den[i] = cval(h->fb, h->dtype, i);
+    } else {
+        for (size_t i = 0; i < nn; ++i) if (num) num[i] = h->c64[i];
+        for (size_t i = 0; i < nd; ++i) if (den) den[i] = h->c64[nn + i];
+    }
+    return SDSP_OK;
+}
+
+// Filter::frequency_response (mod.rs:336-372): Normal = B/A over the stored
+// coefficient vectors; SecondOrder starts from h = 0 and multiplies, so it is 0.
+int sdsp_iir_frequency_response(const sdsp_iir* h, double f, double* re_im) {
+    if (!h || !re_im) return SDSP_E_INVALID_ARGUMENT;
+    if (h->type == 0) {
+        std::vector<cd> b(h->nb), a(h->na - 1);
+        for (int i = 0; i < h->nb; ++i) b[i] = {h->c64[i], 0.0};
+        for (int i = 0; i < h->na - 1; ++i) a[i] = {h->c64[h->nb + i], 0.0};
+        cd r = cdiv(poly_response(b, true, f), poly_response(a, true, f));
+        re_im[0] = r.re;
+        re_im[1] = r.im;
+        return SDSP_OK;
+    }
+    cd acc = {0.0, 0.0};
+    for (int s = 0; s < h->S; ++s) {
+        const double* c = &h->c64[5 * s];
+        // section response (sos.rs:171-190): numerator_coefs = a[1..], denominator_coefs = b
+        std::vector<cd> num = {{c[3], 0.0}, {c[4], 0.0}}, den = {{c[0], 0.0}, {c[1], 0.0}, {c[2], 0.0}};
+        acc = cmul(acc, cdiv(poly_response(num, true, f), poly_response(den, true, f)));
+    }
+    re_im[0] = acc.re;
+    re_im[1] = acc.im;
+    return SDSP_OK;
+}
+
+// Filter::group_delay (mod.rs:392-413; SecondOrderFilter::group_delay sos.rs:208-230)
+int sdsp_iir_group_delay(const sdsp_iir* h, double f, double* delay) {
+    if (!h || !delay) return SDSP_E_INVALID_ARGUMENT;
+    if (h->type == 0) {
+        std::vector<double> b(h->c64.begin(), h->c64.begin() + h->nb), a(h->c64.begin() + h->nb, h->c64.end());
+        double d = 0.0;
+        if (iir_group_delay(b, a, f, &d)) d = 0.0;
+        *delay = d;
+        return SDSP_OK;
+    }
+    double total = 0.0;
+    for (int s = 0; s < h->S; ++s) {
+        const double* c = &h->c64[5 * s];
+        std::vector<double> num = {c[3], c[4]}, den = {c[0], c[1], c[2]};  // swapped names (sos.rs:72-73)
+        double d = 0.0;
+        const double sec = iir_group_delay(num, den, f, &d) ? 0.0 : d + 2.0;
+        total = total + sec + 2.0;
+    }
+    *delay = total;
+    return SDSP_OK;
+}
+
+// SecondOrderFilter accessors (sos.rs:116-150): numerator_coefs = a[1..]/a0, denominator_coefs = b/a0
+int sdsp_sos_section_coefs(const sdsp_iir* h, int section, double* num2, double* den3) {
+    if (!h || h->type != 1 || section < 0 || section >= h->S) return SDSP_E_INVALID_ARGUMENT;
+    const double* c = &h->c64[5 * section];
+    if (num2) { num2[0] = c[3]; num2[1] = c[4]; }
+    if (den3) { den3[0] = c[0]; den3[1] = c[1]; den3[2] = c[2]; }
+    return SDSP_OK;
+}
+
+int sdsp_iir_synchronize(sdsp_iir* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuardI g(h->device);
+    IIR_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+}  // extern "C"

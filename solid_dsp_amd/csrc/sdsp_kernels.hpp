@@ -30,6 +30,11 @@ struct OlsPlan {
     void* d_tw1;  // [256][16] c32: W4096^(t*k)
     void* d_tw2;  // [16][16]  c32: W256^(a*b)
     int halo_rows;  // h2: halo = 256*h2 >= L-1
+    bool wide;        // 16-byte lane-pair global loads/stores
+    bool interleave;  // segment order across the persistent grid
+    bool depth2;      // two segments of loads in flight (8-byte path)
+    bool nomem;       // profiling ablation: arithmetic only, no HBM traffic (outputs invalid)
+    int occ;          // 0: 2-wave kernel; 3/4: occupancy kernel, blocks per CU
 };
 constexpr int kOlsN = 4096;
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
@@ -47,6 +52,25 @@ struct PfbArgs {
 };
 hipError_t launch_pfb(int dtype, const PfbArgs& a, hipStream_t s);
 
+// IIR: SOS cascade (sections > 0) or Normal DF-II (sections == 0)
+struct IirArgs {
+    const void* x;
+    void* y;
+    const void* coefs;   // SOS: [S][5] (b0,b1,b2,a1,a2)/a0 ; Normal: num[nb] then den[na-1]
+    const void* P;       // scan: [8][2S][2S] A^(B 2^k) (Coef type)
+    const void* st_in;   // [channels][state]
+    void* st_out;
+    size_t n, nout, channels;
+    int sections, nb, na, cap;
+    int Mi, Md;          // interpolation (zero stuffing) / decimation factors
+    size_t phase;        // DecimatingIIRFilter index before this block
+    bool algo_scan;
+    int wc;              // warm-up chunks (scan)
+};
+hipError_t launch_iir(int dtype, const IirArgs& a, hipStream_t s);
+int iir_scan_chunk(int dtype);  // samples per lane chunk of the scan kernel
+
+hipError_t launch_bw_copy(const void* a, void* b, size_t bytes, int num_cus, hipStream_t s);
 hipError_t launch_synth_f32(float* out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,
                             hipStream_t s);
 

@@ -36,10 +36,9 @@ from .fir import FIRFilter, DecimatingFIRFilter, PolyPhaseFilterBank, Interpolat
 for _cls in (FIRFilter, DecimatingFIRFilter, InterpolatingFIRFilter):
     Filter.register(_cls)
 
-try:  # IIR family (registered when the library exports it)
-    from . import iir  # noqa: F401
-    from .iir import IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter, InterpolatingIIRFilter  # noqa
-    for _cls in (IIRFilter, DecimatingIIRFilter, InterpolatingIIRFilter):
-        Filter.register(_cls)
-except ImportError:  # pragma: no cover
-    pass
+from . import iir  # noqa: E402,F401
+from .iir import (IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter,  # noqa: E402,F401
+                  InterpolatingIIRFilter)
+
+for _cls in (IIRFilter, DecimatingIIRFilter, InterpolatingIIRFilter):
+    Filter.register(_cls)

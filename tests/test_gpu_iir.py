@@ -1,0 +1,235 @@
+"""GPU parity tests for the IIR family (IIRFilter Normal / SecondOrder,
+SecondOrderFilter, DecimatingIIRFilter, InterpolatingIIRFilter) against the CPU
+restatement.  Serial (EXACT) kernels are bit-identical to the restatement at
+the same precision; the block-parallel scan is checked against the f64
+restatement with the §8d IIR tolerance: rel_RMS <= 1e-5 and
+max|err| <= 1e-5 * max|y_ref|."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from gpu_util import bits_equal, rel_rms
+
+pytestmark = pytest.mark.gpu
+
+sd = pytest.importorskip("solid_dsp_amd")
+from solid_dsp_amd import (IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter,  # noqa: E402
+                           InterpolatingIIRFilter)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ACTIVE_LAG = (0.02, 1.0 / math.sqrt(2.0), 1000.0)
+SO, NORMAL = IIRFilterType.SecondOrder, IIRFilterType.Normal
+IIR_BLOCK = [0.05816769596076701, 0.119535296293297, 0.18410279587774706,
+             0.2518701895942824, 0.32283747232307686]
+DT = [(O.RR32, np.float32, np.float32), (O.RC32, np.float32, np.complex64),
+      (O.RR64, np.float64, np.float64), (O.RC64, np.float64, np.complex128)]
+
+
+def butter():
+    sos = np.array(json.load(open(os.path.join(HERE, "golden", "butter8_0p2_sos.json")))["sos"])
+    return sos[:, :3].reshape(-1), sos[:, 3:].reshape(-1)
+
+
+def rand(rng, n, dt):
+    if np.dtype(dt).kind == "c":
+        return (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(dt)
+    return rng.standard_normal(n).astype(dt)
+
+
+# ---------------------------------------------------------------- KATs
+def test_iir_kats_through_device():
+    n, d = O.active_lag(*ACTIVE_LAG)
+    f = IIRFilter(n, d, SO, sample_dtype=np.float64)
+    assert f.execute(1.0) == [0.05816769596076701]  # mod.rs:262-267
+    f = IIRFilter(n, d, SO, sample_dtype=np.float64)
+    assert list(f.execute_block(np.array([1.0, 0, 1, 0, 1]))) == IIR_BLOCK  # mod.rs:302-307
+    assert f.frequency_response(0.0) == 0j  # mod.rs:334
+    assert f.group_delay(0.0) == 19.6774211296624  # mod.rs:390
+
+
+def test_sos_kats_through_device():  # sos.rs:85-90, 127-129, 147-149, 206
+    n, d = O.active_lag(*ACTIVE_LAG)
+    s = SecondOrderFilter(n, d)
+    assert s.execute(1.0) == 0.05816769596076701
+    assert s.numerator_coefs()[1] == 0.99999840000128
+    assert s.denominator_coefs()[1] == 0.003199997440002048
+    assert s.group_delay(0.0) == 17.6774211296624
+
+
+def test_decim_interp_iir_kats():  # decim.rs:215-219, interp.rs:178-181
+    n, d = O.active_lag(*ACTIVE_LAG)
+    f = DecimatingIIRFilter(n, d, SO, 2, sample_dtype=np.float64)
+    assert list(f.execute_block(np.array([1.0, 0, 1, 0, 1]))) == [0.119535296293297, 0.2518701895942824]
+    g = InterpolatingIIRFilter(n, d, SO, 2, sample_dtype=np.float64)
+    assert g.execute(1.0) == [0.05816769596076701, 0.119535296293297]
+
+
+def test_iir_errors_mirror_reference():
+    with pytest.raises(sd.SdspError) as e:
+        IIRFilter([], [1.0], NORMAL)
+    assert e.value.code == 10
+    with pytest.raises(sd.SdspError) as e:
+        IIRFilter([1.0], [], NORMAL)
+    assert e.value.code == 11
+    with pytest.raises(sd.SdspError) as e:
+        IIRFilter([], [], SO)
+    assert e.value.code == 12
+    with pytest.raises(sd.SdspError) as e:
+        IIRFilter([1.0, 2, 3], [1.0], SO)
+    assert e.value.code == 13
+    with pytest.raises(sd.SdspError) as e:
+        IIRFilter([1.0, 2], [1.0, 2], SO)
+    assert e.value.code == 14
+    with pytest.raises(sd.SdspError) as e:
+        DecimatingIIRFilter([1.0, 2, 3], [1.0, 0, 0], SO, 0)
+    assert e.value.code == 15
+    with pytest.raises(sd.SdspError) as e:
+        InterpolatingIIRFilter([1.0, 2, 3], [1.0, 0, 0], SO, 0)
+    assert e.value.code == 16
+    with pytest.raises(sd.SdspError) as e:
+        SecondOrderFilter([1.0, 2], [1.0, 2, 3])
+    assert e.value.code == 20
+
+
+def test_coefficient_accessors():
+    n, d = O.active_lag(*ACTIVE_LAG)
+    f = IIRFilter(n, d, SO, sample_dtype=np.float64)
+    assert np.array_equal(f.numerator_coefs(), n) and np.array_equal(f.denominator_coefs(), d)
+    g = IIRFilter(n, d, NORMAL, sample_dtype=np.float64)
+    assert np.array_equal(g.numerator_coefs(), n / d[0])
+    assert np.array_equal(g.denominator_coefs(), d[1:] / d[0])
+
+
+# ---------------------------------------------------------------- serial exact parity
+def _sos_random(rng, S, dt):
+    """random stable sections (poles inside |z| < 0.95), unnormalised a0"""
+    ff, fb = [], []
+    for _ in range(S):
+        r, th = rng.uniform(0.2, 0.95), rng.uniform(0, np.pi)
+        a0 = rng.uniform(0.5, 2.0)
+        fb += [a0, -2 * r * np.cos(th) * a0, r * r * a0]
+        ff += list(rng.standard_normal(3))
+    return np.array(ff, dtype=dt), np.array(fb, dtype=dt)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", DT)
+@pytest.mark.parametrize("S", [1, 2, 4, 9])
+@pytest.mark.parametrize("mode,M", [(0, 1), (1, 3), (2, 2)])
+def test_sos_serial_bit_parity(dt, cdt, sdt, S, mode, M):
+    rng = np.random.default_rng(S * 10 + dt + mode)
+    ff, fb = _sos_random(rng, S, cdt)
+    x = rand(rng, 900, sdt)
+    cls = [IIRFilter, DecimatingIIRFilter, InterpolatingIIRFilter][mode]
+    args = (ff, fb, SO) if mode == 0 else (ff, fb, SO, M)
+    f = cls(*args, sample_dtype=sdt, algo=sd.ALGO_EXACT)
+    o = [O.iir(dt, ff, fb, O.SECOND_ORDER), O.iir_decim(dt, ff, fb, O.SECOND_ORDER, M),
+         O.iir_interp(dt, ff, fb, O.SECOND_ORDER, M)][mode]
+    for a, b in [(0, 1), (1, 2), (2, 300), (300, 300), (300, 900)]:
+        assert bits_equal(f.execute_block(x[a:b]), o.execute_block(x[a:b])), (a, b)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", DT)
+@pytest.mark.parametrize("nb,na", [(1, 1), (3, 3), (5, 2), (2, 7), (11, 11)])
+def test_normal_serial_bit_parity(dt, cdt, sdt, nb, na):
+    rng = np.random.default_rng(nb * 31 + na + dt)
+    ff = rng.standard_normal(nb).astype(cdt)
+    # stable denominator: product of first-order sections with |p| < 0.8
+    poly = np.array([1.0])
+    for _ in range(na - 1):
+        poly = np.convolve(poly, [1.0, -rng.uniform(-0.8, 0.8)])
+    fb = (poly * rng.uniform(0.5, 2.0)).astype(cdt)
+    x = rand(rng, 600, sdt)
+    f = IIRFilter(ff, fb, NORMAL, sample_dtype=sdt, algo=sd.ALGO_EXACT)
+    o = O.iir(dt, ff, fb, O.NORMAL)
+    assert bits_equal(f.execute_block(x[:250]), o.execute_block(x[:250]))
+    assert bits_equal(f.execute_block(x[250:]), o.execute_block(x[250:]))
+    if dt == O.RR64:
+        for fr in (0.0, 0.1, 0.3):
+            # bit comparison so NaN responses (na == 1: empty denominator) compare equal
+            assert bits_equal(np.array([f.frequency_response(fr)]), np.array([o.frequency_response(fr)]))
+            assert bits_equal(np.array([f.group_delay(fr)]), np.array([o.group_delay(fr)]))
+
+
+def test_decim_normal_interp_normal():
+    rng = np.random.default_rng(77)
+    ff, fb = rng.standard_normal(4), np.array([1.0, -0.5, 0.1])
+    x = rng.standard_normal(200)
+    f = DecimatingIIRFilter(ff, fb, NORMAL, 4, sample_dtype=np.float64)
+    assert bits_equal(f.execute_block(x), O.iir_decim(O.RR64, ff, fb, O.NORMAL, 4).execute_block(x))
+    g = InterpolatingIIRFilter(ff, fb, NORMAL, 3, sample_dtype=np.float64)
+    assert bits_equal(g.execute_block(x), O.iir_interp(O.RR64, ff, fb, O.NORMAL, 3).execute_block(x))
+
+
+def test_integrator_pole_falls_back_to_exact():
+    # active_lag has a pole at z = 1: no warm-up can make A^W small, the scan is not admissible
+    n, d = O.active_lag(*ACTIVE_LAG)
+    n, d = n.astype(np.float32), d.astype(np.float32)
+    f = IIRFilter(n, d, SO, sample_dtype=np.float32)
+    assert f.scan_info()[0] == 0
+    x = O.synth(3, 0, 0, 50000)
+    assert bits_equal(f.execute_block(x), O.iir(O.RR32, n, d, O.SECOND_ORDER).execute_block(x))
+
+
+# ---------------------------------------------------------------- block-parallel scan
+@pytest.mark.parametrize("dt,cdt,sdt", DT)
+def test_scan_cfg3_cascade_tolerance(dt, cdt, sdt):
+    ff, fb = butter()
+    f = IIRFilter(ff.astype(cdt), fb.astype(cdt), SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    wc, chunk = f.scan_info()
+    assert wc > 0
+    n = 300000
+    x = O.synth(20250226, 3, 0, n, complex_=np.dtype(sdt).kind == "c").astype(sdt)
+    parts = [0, 7, 70000, 70001, 200000, n]
+    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(parts[:-1], parts[1:])])
+    wide = np.complex128 if np.dtype(sdt).kind == "c" else np.float64
+    ref = O.iir(O.RC64 if np.dtype(sdt).kind == "c" else O.RR64, ff.astype(cdt).astype(np.float64),
+                fb.astype(cdt).astype(np.float64), O.SECOND_ORDER).execute_block(x.astype(wide))
+    tol = 1e-5 if cdt == np.float32 else 1e-12
+    assert rel_rms(y, ref) <= tol
+    assert np.abs(y - ref).max() <= tol * np.abs(ref).max()
+
+
+def test_scan_decim_interp_and_state_carry():
+    ff, fb = butter()
+    x = O.synth(11, 0, 0, 100000)
+    f = DecimatingIIRFilter(ff, fb, SO, 5, sample_dtype=np.float64, algo=sd.ALGO_FMA)
+    y = np.concatenate([f.execute_block(x[:33333]), f.execute_block(x[33333:])])
+    ref = O.iir_decim(O.RR64, ff, fb, O.SECOND_ORDER, 5).execute_block(x.astype(np.float64))
+    assert rel_rms(y, ref) <= 1e-12
+    g = InterpolatingIIRFilter(ff, fb, SO, 3, sample_dtype=np.float64, algo=sd.ALGO_FMA)
+    y = g.execute_block(x[:40000])
+    ref = O.iir_interp(O.RR64, ff, fb, O.SECOND_ORDER, 3).execute_block(x[:40000].astype(np.float64))
+    assert rel_rms(y, ref) <= 1e-12
+
+
+def test_scan_multichannel_and_clone():
+    import torch
+    ff, fb = butter()
+    ch, n = 4, 50000
+    x = np.stack([O.synth(5, c, 0, n) for c in range(ch)])
+    f = IIRFilter(ff.astype(np.float32), fb.astype(np.float32), SO, sample_dtype=np.float32, channels=ch,
+                  algo=sd.ALGO_FMA)
+    y1 = f.execute_block(x[:, : n // 2].copy())
+    g = f.clone()
+    y2 = f.execute_block(x[:, n // 2:].copy())
+    y2c = g.execute_block(x[:, n // 2:].copy())
+    assert bits_equal(y2, y2c)
+    for c in range(ch):
+        ref = O.iir(O.RR64, ff.astype(np.float32).astype(np.float64), fb.astype(np.float32).astype(np.float64),
+                    O.SECOND_ORDER).execute_block(x[c].astype(np.float64))
+        assert rel_rms(np.concatenate([y1[c], y2[c]]), ref) <= 1e-5
+
+
+def test_get_set_state_roundtrip():
+    ff, fb = butter()
+    x = O.synth(8, 0, 0, 20000).astype(np.float64)
+    f = IIRFilter(ff, fb, SO, sample_dtype=np.float64, algo=sd.ALGO_EXACT)
+    f.execute_block(x[:10000])
+    st, ph = f.get_state()
+    g = IIRFilter(ff, fb, SO, sample_dtype=np.float64, algo=sd.ALGO_EXACT)
+    g.set_state(st, ph)
+    assert bits_equal(f.execute_block(x[10000:]), g.execute_block(x[10000:]))

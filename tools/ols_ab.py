@@ -1,0 +1,60 @@
+"""Interleaved in-process A/B of overlap-save kernel variants (guide §5.4 rule 24).
+Outputs of every variant must be bit-identical."""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main(rounds=8, log2n=30):
+    import torch
+    import solid_dsp_amd as sd
+    from solid_dsp_amd import FIRFilter
+    from solid_dsp_amd.filter import firdes
+    n = 1 << log2n
+    h = firdes.firdes_kaiser(256, 0.1, 80.0, 0.0).astype(np.float32)
+    d_in = torch.empty(n, dtype=torch.complex64, device="cuda")
+    sd.lib().sdsp_synth_f32_device(d_in.data_ptr(), 20250226, 0, 0, 2 * n, None)
+    outs = {}
+    variants = {}
+    cfgs = json.loads(os.environ.get("OLS_VARIANTS", "[[0,1,0,0],[0,1,0,1]]"))
+    for cfg in cfgs:
+        wide, inter, d2, nomem = cfg[:4]
+        occ = cfg[4] if len(cfg) > 4 else 0
+        f = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, algo=sd.ALGO_FFT)
+        sd.lib().sdsp_fir_set_tuning(f._h, 1, wide)
+        sd.lib().sdsp_fir_set_tuning(f._h, 2, inter)
+        sd.lib().sdsp_fir_set_tuning(f._h, 3, d2)
+        sd.lib().sdsp_fir_set_tuning(f._h, 4, nomem)
+        sd.lib().sdsp_fir_set_tuning(f._h, 5, occ)
+        variants[f"wide{wide}_inter{inter}_d2{d2}_occ{occ}_nomem{nomem}"] = f
+    s = torch.cuda.current_stream()
+    times = {k: [] for k in variants}
+    for k, f in variants.items():
+        o = torch.empty_like(d_in)
+        f.reset()
+        f.execute_block_device(d_in, n, o, s)
+        outs[k] = o[: 1 << 22].cpu().numpy().copy(), o[-(1 << 20):].cpu().numpy().copy()
+        del o
+    ref = outs[next(k for k in outs if k.endswith("nomem0"))]
+    same = {k: bool(np.array_equal(v[0].view(np.uint64), ref[0].view(np.uint64)) and
+                    np.array_equal(v[1].view(np.uint64), ref[1].view(np.uint64))) for k, v in outs.items()}
+    d_out = torch.empty_like(d_in)
+    for r in range(rounds):
+        for k, f in variants.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            f.execute_block_device(d_in, n, d_out, s)
+            e1.record(s)
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1))
+    res = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
+               "GBps": 16.0 * n / (np.median(v) * 1e-3) / 1e9, "identical": same[k]} for k, v in times.items()}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
