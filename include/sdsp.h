@@ -247,6 +247,50 @@ SDSP_API int sdsp_iir_group_delay(const sdsp_iir* h, double f, double* delay);
 SDSP_API int sdsp_iir_synchronize(sdsp_iir* h);
 
 /* ------------------------------------------------------------------------
+ * FFT  (FFT::new / FFT::execute, src/fft/mod.rs:175-215).  direction: 0 FORWARD,
+ * 1 REVERSE (unnormalised, like the reference).  precision: 0 = complex f32,
+ * 1 = complex f64.  Power-of-two sizes up to 4096 run a radix-4 Stockham FFT in
+ * LDS; other sizes a direct DFT.
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_fft sdsp_fft;
+SDSP_API int sdsp_fft_create(sdsp_fft** out, size_t nfft, int direction, int precision, int device);
+SDSP_API void sdsp_fft_destroy(sdsp_fft* h);
+SDSP_API size_t sdsp_fft_len(const sdsp_fft* h);
+/* `batch` contiguous transforms of nfft complex samples */
+SDSP_API int sdsp_fft_execute(sdsp_fft* h, const void* in, void* out, size_t batch);
+SDSP_API int sdsp_fft_execute_device(sdsp_fft* h, const void* d_in, void* d_out, size_t batch, void* stream);
+
+/* ------------------------------------------------------------------------
+ * PFB + FFT channeliser (build-defined composition of PolyPhaseFilterBank's
+ * coefficient layout, src/filter/fir/pfb.rs:24-49, and FFT FORWARD; SURVEY
+ * Appendix A.6).  M channels (power of two, 4..4096), K = len / M taps per
+ * branch, branch p fed by input phase M-1-p.  dtype SDSP_RC32 or SDSP_RC64.
+ * Blocks are whole frames: n (per stream) a multiple of M; out[s][frame][M].
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_chan sdsp_chan;
+SDSP_API int sdsp_chan_create(sdsp_chan** out, int dtype, const void* taps, size_t len, size_t channels,
+                              int device);
+SDSP_API void sdsp_chan_destroy(sdsp_chan* h);
+SDSP_API int sdsp_chan_set_streams(sdsp_chan* h, size_t streams);
+SDSP_API int sdsp_chan_reset(sdsp_chan* h);
+SDSP_API int sdsp_chan_execute_block(sdsp_chan* h, const void* in, size_t n, void* out, size_t* frames);
+SDSP_API int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, void* d_out,
+                                            size_t* frames, void* stream);
+SDSP_API int sdsp_chan_synchronize(sdsp_chan* h);
+
+/* ------------------------------------------------------------------------
+ * DotProduct (src/dot_product/mod.rs:37-171): DotProduct::new(&coefs, direction)
+ * + Execute::execute(&samples), reference order (bit-identical).  direction:
+ * 0 FORWARD, 1 REVERSE.  The batched form runs `batch` sample vectors of n
+ * samples spaced `stride` samples apart (device pointers, current device).
+ * ------------------------------------------------------------------------ */
+SDSP_API int sdsp_dot_execute(int dtype, const void* coefs, size_t len, int direction, const void* samples,
+                              size_t n, void* out);
+SDSP_API int sdsp_dot_execute_batched_device(int dtype, const void* coefs, size_t len, int direction,
+                                             const void* d_samples, size_t n, size_t stride, size_t batch,
+                                             void* d_out, void* stream);
+
+/* ------------------------------------------------------------------------
  * Device utilities
  * ------------------------------------------------------------------------ */
 /* Synthetic stream (build-defined): `count` f32 scalars

@@ -8,7 +8,10 @@ arguments, error codes).  There is no CPU execution path.
 """
 from ._lib import (SdspError, lib, LIB_PATH, RR32, RC32, CC32, RR64, RC64, CC64,  # noqa: F401
                    ALGO_AUTO, ALGO_EXACT, ALGO_FMA, ALGO_FFT)
-from . import filter, group_delay  # noqa: F401
+from . import filter, group_delay, fft, dot_product, channelizer  # noqa: F401
+from .fft import FFT, FFTDirection, FFTFlags  # noqa: F401
+from .dot_product import DotProduct, Direction  # noqa: F401
+from .channelizer import Channelizer  # noqa: F401
 from .filter import (Filter, FIRFilter, DecimatingFIRFilter, PolyPhaseFilterBank,  # noqa: F401
                      InterpolatingFIRFilter, IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter,
                      InterpolatingIIRFilter)

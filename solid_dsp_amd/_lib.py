@@ -162,18 +162,19 @@ def _optional_sigs():
         "sdsp_iir_scan_info": (i, [vp, i, C.POINTER(i), C.POINTER(i)]),
         "sdsp_sos_section_coefs": (i, [vp, i, dp, dp]),
         "sdsp_sos_create": (i, [vpp, C.POINTER(C.c_double), sz, C.POINTER(C.c_double), sz, i]),
-        "sdsp_chan_create": (i, [vpp, vp, sz, sz, i]),
+        "sdsp_chan_create": (i, [vpp, i, vp, sz, sz, i]),
         "sdsp_chan_destroy": (None, [vp]),
         "sdsp_chan_set_streams": (i, [vp, sz]),
         "sdsp_chan_execute_block_device": (i, [vp, vp, sz, vp, szp, vp]),
         "sdsp_chan_execute_block": (i, [vp, vp, sz, vp, szp]),
         "sdsp_chan_reset": (i, [vp]),
         "sdsp_chan_synchronize": (i, [vp]),
-        "sdsp_fft_create": (i, [vpp, sz, i, i]),
+        "sdsp_fft_create": (i, [vpp, sz, i, i, i]),
         "sdsp_fft_destroy": (None, [vp]),
         "sdsp_fft_execute": (i, [vp, vp, vp, sz]),
         "sdsp_fft_execute_device": (i, [vp, vp, vp, sz, vp]),
-        "sdsp_dot_execute_batched_device": (i, [i, vp, sz, i, vp, sz, sz, vp, vp]),
+        "sdsp_dot_execute_batched_device": (i, [i, vp, sz, i, vp, sz, sz, sz, vp, vp]),
+        "sdsp_fft_len": (sz, [vp]),
         "sdsp_dot_execute": (i, [i, vp, sz, i, vp, sz, vp]),
     }
 

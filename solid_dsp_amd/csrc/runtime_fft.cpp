@@ -1,0 +1,335 @@
+// C-ABI runtime for FFT (src/fft/mod.rs:175-215), the PFB + FFT channeliser
+// (build-defined) and batched DotProduct::execute
+// (src/dot_product/mod.rs:153-171).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "sdsp.h"
+#include "sdsp_host.hpp"
+#include "sdsp_kernels.hpp"
+
+using namespace sdsp;
+
+namespace {
+
+#define F_TRY(expr, what)                                      \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return device_status(_e, what);  \
+    } while (0)
+
+struct Guard {
+    int prev = -1;
+    explicit Guard(int d) {
+        (void)hipGetDevice(&prev);
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~Guard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int check_gfx950(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) {
+        set_error("no HIP device visible (libsdsp has no CPU execution path)");
+        return SDSP_E_NO_DEVICE;
+    }
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess || std::strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+        set_error("libsdsp is built for gfx950");
+        return SDSP_E_NO_DEVICE;
+    }
+    return SDSP_OK;
+}
+
+bool is_pow2(size_t n) { return n && !(n & (n - 1)); }
+int ilog2(size_t n) {
+    int l = 0;
+    while ((size_t)1 << l < n) ++l;
+    return l;
+}
+
+// e^{-j 2 pi m / N}, computed in f64, stored as c32 or c64
+int make_twiddles(DevBuf& buf, size_t N, bool f64) {
+    std::vector<double> w(2 * N);
+    for (size_t m = 0; m < N; ++m) {
+        const double a = -2.0 * M_PI * (double)m / (double)N;
+        w[2 * m] = std::cos(a);
+        w[2 * m + 1] = std::sin(a);
+    }
+    if (f64) {
+        F_TRY(buf.ensure(w.size() * 8), "alloc twiddles");
+        F_TRY(hipMemcpy(buf.p, w.data(), w.size() * 8, hipMemcpyHostToDevice), "copy twiddles");
+    } else {
+        std::vector<float> f(w.begin(), w.end());
+        F_TRY(buf.ensure(f.size() * 4), "alloc twiddles");
+        F_TRY(hipMemcpy(buf.p, f.data(), f.size() * 4, hipMemcpyHostToDevice), "copy twiddles");
+    }
+    return SDSP_OK;
+}
+
+}  // namespace
+
+struct sdsp_fft {
+    size_t N = 0;
+    int direction = 0;  // 0 FORWARD, 1 REVERSE
+    bool f64 = true;
+    int device = 0;
+    DevBuf tw, stage_in, stage_out;
+    hipStream_t stream = nullptr;
+};
+
+struct sdsp_chan {
+    int dtype = SDSP_RC32, device = 0;
+    size_t M = 0, K = 0, streams = 1;
+    std::vector<unsigned char> taps;
+    DevBuf cb, tw, hist[2], stage_in, stage_out;
+    int cur = 0;
+    hipStream_t stream = nullptr;
+};
+
+extern "C" {
+
+// FFT::new(nfft, direction, flags)   src/fft/mod.rs:175-186
+int sdsp_fft_create(sdsp_fft** out, size_t nfft, int direction, int precision, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (nfft == 0 || nfft > (1u << 24)) {  // the reference panics on a zero-length plan
+        set_error("FFT size must be in [1, 2^24]");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    if (direction != 0 && direction != 1) return SDSP_E_INVALID_ARGUMENT;
+    if (is_pow2(nfft) && nfft > 4096) {
+        set_error("power-of-two FFT sizes above 4096 are not supported on the device yet");
+        return SDSP_E_UNSUPPORTED;
+    }
+    int st = check_gfx950(device);
+    if (st) return st;
+    Guard g(device);
+    sdsp_fft* h = new sdsp_fft();
+    h->N = nfft;
+    h->direction = direction;
+    h->f64 = precision != 0;
+    h->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete h; return device_status(e, "stream"); }
+    st = make_twiddles(h->tw, nfft, h->f64);
+    if (st) { sdsp_fft_destroy(h); return st; }
+    *out = h;
+    return SDSP_OK;
+}
+
+void sdsp_fft_destroy(sdsp_fft* h) {
+    if (!h) return;
+    {
+        Guard g(h->device);
+        if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
+        h->tw.release();
+        h->stage_in.release();
+        h->stage_out.release();
+    }
+    delete h;
+}
+
+size_t sdsp_fft_len(const sdsp_fft* h) { return h ? h->N : 0; }
+
+int sdsp_fft_execute_device(sdsp_fft* h, const void* d_in, void* d_out, size_t batch, void* stream) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (batch == 0) return SDSP_OK;
+    if (d_in == d_out && !is_pow2(h->N)) {
+        set_error("in-place direct DFT is not supported");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    Guard g(h->device);
+    FftArgs a{d_in, d_out, h->tw.p, (int)h->N, ilog2(h->N), is_pow2(h->N), h->direction == 1, batch};
+    F_TRY(launch_fft(h->f64, a, stream ? (hipStream_t)stream : h->stream), "fft");
+    return SDSP_OK;
+}
+
+// FFT::execute(&[Complex]) -> Vec<Complex> over `batch` contiguous transforms   src/fft/mod.rs:188-215
+int sdsp_fft_execute(sdsp_fft* h, const void* in, void* out, size_t batch) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (batch == 0) return SDSP_OK;
+    Guard g(h->device);
+    const size_t bytes = h->N * batch * (h->f64 ? 16 : 8);
+    F_TRY(h->stage_in.ensure(bytes), "stage");
+    F_TRY(h->stage_out.ensure(bytes), "stage");
+    F_TRY(hipMemcpyAsync(h->stage_in.p, in, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    int st = sdsp_fft_execute_device(h, h->stage_in.p, h->stage_out.p, batch, h->stream);
+    if (st) return st;
+    F_TRY(hipMemcpyAsync(out, h->stage_out.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+    F_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+// ---- channeliser -----------------------------------------------------------
+int sdsp_chan_create(sdsp_chan** out, int dtype, const void* taps, size_t len, size_t M, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (dtype != SDSP_RC32 && dtype != SDSP_RC64) {
+        set_error("channeliser takes real taps and complex samples (SDSP_RC32 / SDSP_RC64)");
+        return SDSP_E_UNSUPPORTED;
+    }
+    if (M == 0) { set_error("FIR Filter Error NotEnoughFilters"); return SDSP_E_NOT_ENOUGH_FILTERS; }
+    if (len == 0) { set_error("FIR Filter Error CoefficientsLengthZero"); return SDSP_E_COEFFICIENTS_LENGTH_ZERO; }
+    if (!is_pow2(M) || M < 4 || M > 4096) {
+        set_error("channel count must be a power of two in [4, 4096]");
+        return SDSP_E_UNSUPPORTED;
+    }
+    const size_t K = len / M;
+    if (K == 0) { set_error("fewer taps than channels"); return SDSP_E_INVALID_ARGUMENT; }
+    int st = check_gfx950(device);
+    if (st) return st;
+    Guard g(device);
+    sdsp_chan* h = new sdsp_chan();
+    h->dtype = dtype;
+    h->device = device;
+    h->M = M;
+    h->K = K;
+    const size_t cbytes = coef_bytes(dtype);
+    h->taps.assign((const unsigned char*)taps, (const unsigned char*)taps + len * cbytes);
+    // branch coefficients, stored order: cb[p][K-1-idx] = h[p + idx M]   (pfb.rs:33-40)
+    std::vector<unsigned char> cb(M * K * cbytes);
+    for (size_t p = 0; p < M; ++p)
+        for (size_t idx = 0; idx < K; ++idx)
+            std::memcpy(&cb[(p * K + (K - 1 - idx)) * cbytes], &h->taps[(p + idx * M) * cbytes], cbytes);
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = h->cb.ensure(cb.size());
+    if (e == hipSuccess) e = hipMemcpy(h->cb.p, cb.data(), cb.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { st = device_status(e, "chan create"); sdsp_chan_destroy(h); return st; }
+    st = make_twiddles(h->tw, M, dtype == SDSP_RC64);
+    if (!st) st = sdsp_chan_set_streams(h, 1);
+    if (st) { sdsp_chan_destroy(h); return st; }
+    *out = h;
+    return SDSP_OK;
+}
+
+void sdsp_chan_destroy(sdsp_chan* h) {
+    if (!h) return;
+    {
+        Guard g(h->device);
+        if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
+        h->cb.release(); h->tw.release(); h->hist[0].release(); h->hist[1].release();
+        h->stage_in.release(); h->stage_out.release();
+    }
+    delete h;
+}
+
+int sdsp_chan_set_streams(sdsp_chan* h, size_t streams) {
+    if (!h || streams == 0) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    h->streams = streams;
+    const size_t hb = streams * (h->K - 1) * h->M * sample_bytes(h->dtype);
+    for (int i = 0; i < 2; ++i) {
+        F_TRY(h->hist[i].ensure(hb), "alloc history");
+        if (hb) F_TRY(hipMemsetAsync(h->hist[i].p, 0, hb, h->stream), "zero history");
+    }
+    h->cur = 0;
+    F_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_chan_reset(sdsp_chan* h) { return h ? sdsp_chan_set_streams(h, h->streams) : SDSP_E_INVALID_ARGUMENT; }
+
+int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, void* d_out, size_t* frames,
+                                   void* stream) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (n % h->M) {
+        set_error("channeliser blocks must be a whole number of M-sample frames");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    const size_t fr = n / h->M;
+    if (frames) *frames = fr;
+    if (fr == 0) return SDSP_OK;
+    Guard g(h->device);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    ChanArgs a{d_in, h->hist[h->cur].p, h->cb.p, d_out, h->tw.p, (int)h->M, ilog2(h->M), (int)h->K, n, fr, h->streams};
+    F_TRY(launch_chan(h->dtype == SDSP_RC64, a, s), "channeliser");
+    const int H = (int)((h->K - 1) * h->M);
+    F_TRY(launch_hist_update(h->dtype, d_in, h->hist[h->cur].p, h->hist[h->cur ^ 1].p, n, H, h->streams, s),
+          "history update");
+    h->cur ^= 1;
+    return SDSP_OK;
+}
+
+int sdsp_chan_execute_block(sdsp_chan* h, const void* in, size_t n, void* out, size_t* frames) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    const size_t bytes = h->streams * n * sample_bytes(h->dtype);
+    if (n % h->M) {
+        set_error("channeliser blocks must be a whole number of M-sample frames");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    if (frames) *frames = n / h->M;
+    if (n == 0) return SDSP_OK;
+    F_TRY(h->stage_in.ensure(bytes), "stage");
+    F_TRY(h->stage_out.ensure(bytes), "stage");
+    F_TRY(hipMemcpyAsync(h->stage_in.p, in, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    int st = sdsp_chan_execute_block_device(h, h->stage_in.p, n, h->stage_out.p, nullptr, h->stream);
+    if (st) return st;
+    F_TRY(hipMemcpyAsync(out, h->stage_out.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+    F_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_chan_synchronize(sdsp_chan* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    F_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+// ---- DotProduct ---------------------------------------------------------------
+// batch vectors of n samples (stride samples apart), coefficients as given to
+// DotProduct::new(&coefs, direction) (0 FORWARD, 1 REVERSE), device buffers.
+int sdsp_dot_execute_batched_device(int dtype, const void* coefs, size_t len, int direction, const void* d_samples,
+                                    size_t n, size_t stride, size_t batch, void* d_out, void* stream) {
+    if (dtype < 0 || dtype > 5 || direction < 0 || direction > 1) return SDSP_E_INVALID_ARGUMENT;
+    if (batch == 0) return SDSP_OK;
+    int dev = 0;
+    F_TRY(hipGetDevice(&dev), "device");
+    int st = check_gfx950(dev);
+    if (st) return st;
+    const size_t cb = coef_bytes(dtype);
+    std::vector<unsigned char> c((const unsigned char*)coefs, (const unsigned char*)coefs + len * cb);
+    if (direction == 1)
+        for (size_t i = 0; i < len / 2; ++i)
+            std::swap_ranges(&c[i * cb], &c[i * cb] + cb, &c[(len - 1 - i) * cb]);
+    DevBuf d_c;
+    F_TRY(d_c.ensure(c.size()), "alloc coefs");
+    hipStream_t s = (hipStream_t)stream;
+    F_TRY(hipMemcpyAsync(d_c.p, c.data(), c.size(), hipMemcpyHostToDevice, s), "copy coefs");
+    DotArgs a{d_c.p, (int)std::min(n, len), d_samples, stride, batch, d_out};
+    F_TRY(launch_dot(dtype, a, s), "dot");
+    F_TRY(hipStreamSynchronize(s), "sync");  // d_c is released on return
+    return SDSP_OK;
+}
+
+// single DotProduct::execute over host buffers (out = one sample)
+int sdsp_dot_execute(int dtype, const void* coefs, size_t len, int direction, const void* samples, size_t n,
+                     void* out) {
+    if (dtype < 0 || dtype > 5) return SDSP_E_INVALID_ARGUMENT;
+    int dev = 0;
+    F_TRY(hipGetDevice(&dev), "device");
+    int st = check_gfx950(dev);
+    if (st) return st;
+    const size_t sb = sample_bytes(dtype);
+    DevBuf s, o;
+    F_TRY(s.ensure(std::max<size_t>(n, 1) * sb), "alloc");
+    F_TRY(o.ensure(sb), "alloc");
+    if (n) F_TRY(hipMemcpy(s.p, samples, n * sb, hipMemcpyHostToDevice), "H2D");
+    st = sdsp_dot_execute_batched_device(dtype, coefs, len, direction, s.p, n, n, 1, o.p, nullptr);
+    if (st) return st;
+    F_TRY(hipMemcpy(out, o.p, sb, hipMemcpyDeviceToHost), "D2H");
+    return SDSP_OK;
+}
+
+}  // extern "C"

@@ -70,6 +70,39 @@ struct IirArgs {
 hipError_t launch_iir(int dtype, const IirArgs& a, hipStream_t s);
 int iir_scan_chunk(int dtype);  // samples per lane chunk of the scan kernel
 
+// batched FFT (power of two: Stockham in LDS; otherwise direct DFT)
+struct FftArgs {
+    const void* x;
+    void* y;
+    const void* tw;  // [N] e^{-j 2 pi m / N}
+    int N, logN;
+    bool pow2, inverse;
+    size_t batch;
+};
+hipError_t launch_fft(bool f64, const FftArgs& a, hipStream_t s);
+
+// PFB + FFT channeliser (M power of two)
+struct ChanArgs {
+    const void* x;     // [streams][n]
+    const void* hist;  // [streams][(K-1) M]
+    const void* cb;    // [M][K] real branch coefficients (stored order)
+    void* y;           // [streams][frames][M]
+    const void* tw;
+    int M, logM, K;
+    size_t n, frames, streams;
+};
+hipError_t launch_chan(bool f64, const ChanArgs& a, hipStream_t s);
+
+// batched DotProduct::execute
+struct DotArgs {
+    const void* coefs;
+    int it;  // min(samples, len)
+    const void* s;
+    size_t stride, batch;
+    void* out;
+};
+hipError_t launch_dot(int dtype, const DotArgs& a, hipStream_t s);
+
 hipError_t launch_bw_copy(const void* a, void* b, size_t bytes, int num_cus, hipStream_t s);
 hipError_t launch_synth_f32(float* out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,
                             hipStream_t s);

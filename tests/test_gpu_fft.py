@@ -1,0 +1,110 @@
+"""GPU FFT, channeliser and DotProduct parity against the CPU restatement."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from gpu_util import bits_equal, rel_rms, to_dev, empty_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+sd = pytest.importorskip("solid_dsp_amd")
+from solid_dsp_amd import FFT, FFTDirection, DotProduct, Direction, Channelizer  # noqa: E402
+
+
+def offt(x, d):
+    L = O.lib()
+    h = L.orc_fft_new(len(x), d)
+    y = np.zeros(len(x), np.complex128)
+    L.orc_fft_execute(h, O._ptr(np.ascontiguousarray(x, np.complex128)), O._ptr(y))
+    L.orc_fft_free(h)
+    return y
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 3, 5, 12, 100, 257, 1000])
+@pytest.mark.parametrize("prec", [np.complex64, np.complex128])
+def test_fft_vs_restatement(n, prec):
+    rng = np.random.default_rng(n)
+    batch = 3
+    x = (rng.standard_normal((batch, n)) + 1j * rng.standard_normal((batch, n))).astype(prec)
+    for d in (FFTDirection.FORWARD, FFTDirection.REVERSE):
+        y = FFT(n, d, precision=prec).execute(x)
+        for b in range(batch):
+            ref = offt(x[b].astype(np.complex128), int(d))
+            # f32: single-precision FFT; f64: bounded by the reference's own 8-digit DFT16 twiddles
+            tol = 2e-6 if prec == np.complex64 else 1e-7
+            assert rel_rms(y[b], ref) <= tol, (n, d, rel_rms(y[b], ref))
+
+
+def test_fft_errors():
+    with pytest.raises(sd.SdspError):
+        FFT(0)
+
+
+@pytest.mark.parametrize("M,K", [(16, 4), (64, 8), (1024, 8)])
+def test_channelizer_vs_restatement(M, K):
+    rng = np.random.default_rng(M + K)
+    h = O.firdes_kaiser(M * K, 0.5 / M, 80.0, 0.0).astype(np.float32)
+    frames = 12
+    x = O.synth(20250226, 1, 0, M * frames, complex_=True)
+    ch = Channelizer(h, M, sample_dtype=np.complex64)
+    y = np.concatenate([ch.execute_block(x[: 5 * M]), ch.execute_block(x[5 * M:])])
+    ref = np.zeros(M * frames, np.complex128)
+    O.lib().orc_channelize(O._ptr(h.astype(np.float64)), len(h), M, O._ptr(x.astype(np.complex128)), len(x),
+                           O._ptr(ref))
+    ref = ref.reshape(frames, M)
+    assert rel_rms(y, ref) <= 1e-6
+    assert np.abs(y - ref).max() <= 1e-6 * np.abs(h).sum() * np.abs(x).max() * np.sqrt(M)
+
+
+def test_channelizer_multistream_device():
+    import torch
+    M, K, frames, S = 64, 8, 20, 3
+    h = O.firdes_kaiser(M * K, 0.5 / M, 80.0, 0.0)
+    x = np.stack([O.synth(9, s, 0, M * frames, complex_=True).astype(np.complex128) for s in range(S)])
+    ch = Channelizer(h, M, sample_dtype=np.complex128, streams=S)
+    d_in = to_dev(x.reshape(-1))
+    d_out = empty_dev(S * M * frames, np.complex128)
+    assert ch.execute_block_device(d_in, M * frames, d_out, torch.cuda.current_stream()) == frames
+    y = to_host(d_out).reshape(S, frames, M)
+    for s in range(S):
+        ref = np.zeros(M * frames, np.complex128)
+        O.lib().orc_channelize(O._ptr(h), len(h), M, O._ptr(x[s]), M * frames, O._ptr(ref))
+        assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-7
+
+
+@pytest.mark.parametrize("cdt,sdt,kind", [(np.float64, np.float64, 0), (np.float64, np.complex128, 1),
+                                          (np.complex128, np.complex128, 2)])
+@pytest.mark.parametrize("direction", [Direction.FORWARD, Direction.REVERSE])
+def test_dot_product_bit_parity(cdt, sdt, kind, direction):
+    """vs the oracle DotProduct restatement (f64 family), bit for bit"""
+    rng = np.random.default_rng(1)
+    c = rng.standard_normal(37).astype(cdt)
+    if np.dtype(cdt).kind == "c":
+        c = c + 1j * rng.standard_normal(37)
+    for n in (37, 20, 50):  # iterations = min(samples, len)  (mod.rs:161)
+        s = rng.standard_normal(n).astype(sdt)
+        if np.dtype(sdt).kind == "c":
+            s = s + 1j * rng.standard_normal(n)
+        got = DotProduct(c, direction, sample_dtype=sdt).execute(s)
+        ref = np.zeros(2)
+        O.lib().orc_dot_execute(kind, O._ptr(c), len(c), int(direction), O._ptr(s), n, O._dptr(ref))
+        r = ref[0] if kind == 0 else complex(ref[0], ref[1])
+        assert bits_equal(np.array([got], dtype=sdt), np.array([r], dtype=sdt))
+
+
+def test_dot_product_batched_device_f32():
+    import torch
+    rng = np.random.default_rng(2)
+    c = rng.standard_normal(16).astype(np.float32)
+    S = (rng.standard_normal((100, 24)) + 1j * rng.standard_normal((100, 24))).astype(np.complex64)
+    d_s = to_dev(S.reshape(-1))
+    d_o = empty_dev(100, np.complex64)
+    DotProduct(c, Direction.REVERSE, sample_dtype=np.complex64).execute_batched_device(
+        d_s, 24, 24, 100, d_o, torch.cuda.current_stream())
+    got = to_host(d_o)
+    ref = (S[:, :16] * c[::-1].astype(np.float64)).sum(axis=1)
+    assert rel_rms(got, ref) <= 1e-6
+
+
+def test_dot_product_kat():  # src/dot_product/mod.rs:15
+    assert DotProduct(np.array([1.0, 2, 3, 4, 5]), Direction.REVERSE).execute(np.ones(5)) == 15.0
