@@ -1,15 +1,21 @@
 #!/usr/bin/env python3
-"""Headline benchmark: 256-tap complex-f32 FIR over a 1 GiS synthetic stream
-(BASELINE.json configs[1]; metric "Msamples/sec 256-tap complex FIR
-@1/2/4/8 GPU; % HBM roofline").
+"""Benchmarks of the streaming filter engine on MI355X.
 
-One step = one FIRFilter::execute_block pass (device resident, overlap-save
-kernel) over the whole 2^30-sample channel.  With N ranks each rank filters
-its own independent channel (weak scaling, no collective in the timed
-region); RCCL is used afterwards only for the final gather, timed
-separately.  rank 0 prints one JSON line.
+Default (the driver's headline, BASELINE.json configs[1]): 256-tap complex-f32
+FIR over a 1 GiS synthetic stream per GPU, metric "Msamples/sec 256-tap
+complex FIR @1/2/4/8 GPU; % HBM roofline".  One step = one device-resident
+FIRFilter::execute_block pass (overlap-save kernel) over the whole channel.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--log2n 30] [--algo fft|exact|fma]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--log2n 30] [--algo fft|exact|fma]
+
+Other configs (BASELINE.json configs[2..4]):
+  3  4-biquad cascade (scipy butter(8, 0.2) SOS), real f32, 1 GiS, block-parallel scan
+  4  M=32 decimator, 256 taps (32 branches x 8), crcf, 1 GiS input per GPU
+  5  1024-channel PFB + FFT channeliser, 8 streams x 2^24 samples per GPU
+
+With N ranks each rank processes its own independent channel(s) (weak
+scaling, no collective in the timed region); RCCL is used afterwards only for
+the final gather, timed separately.  rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -21,10 +27,10 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level table)
 SEED = 20250226
-TAPS = 256
 
 
 def parse():
@@ -32,59 +38,246 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--log2n", type=int, default=30)
-    p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"])
-    p.add_argument("--cpu-samples", type=int, default=1 << 24,
+    p.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    p.add_argument("--log2n", type=int, default=30, help="samples per GPU per step (configs 2-4)")
+    p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"], help="config 2 kernel")
+    p.add_argument("--cpu-samples", type=int, default=None,
                    help="bounded sample of the same workload timed on the host (oracle restatement)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     return p.parse_args()
 
 
-def load_traffic():
+def load_traffic(config, log2n, algo):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (profiles/*_pmc_summary.json written by tools/pmc_traffic.py), or None."""
+    (profiles/*/pmc_summary_cfg*.json written by tools/pmc_summary.py), or None."""
     import glob
-    best = None
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_summary.json"))):
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_summary_cfg{config}.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            if d.get("kernel_prefix") and d.get("hbm_bytes_per_launch"):
-                best = d
-        except (OSError, ValueError):
+            if d.get("log2n") == log2n and d.get("algo", algo) == algo:
+                return d["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
             pass
-    return best
+    return None
 
 
-def cpu_baseline(h, n_samples):
-    """Time the oracle's restatement of the reference algorithm (f64, like the
-    reference Filter path) on one host core over a bounded sample."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_lib as O
-    x = O.synth(SEED, 0, 0, n_samples, complex_=True).astype(np.complex128)
-    f = O.fir(O.RC64, h.astype(np.float64), 0.2)
+def timed_cpu(fn, label, samples, cores=1):
     t0 = time.perf_counter()
-    f.execute_block(x)
+    fn()
     dt = time.perf_counter() - t0
-    return {"value": n_samples / dt / 1e6, "unit": "Msamples/sec", "cores": 1, "kind": "port",
-            "sample": f"first {n_samples} samples of channel 0, FIRFilter<f64, Complex<f64>> restatement "
-                      f"(memmove Window + to_vec + sequential dot), 1 thread, {dt:.1f} s"}
+    return {"value": samples / dt / 1e6, "unit": "Msamples/sec", "cores": cores, "kind": "port",
+            "sample": f"{label}, {samples} input samples, {cores} thread(s), {dt:.1f} s"}
 
 
-def parity_windows(h, x_dev_host_fetch, y_dev_host_fetch, n, rng, windows=4, width=4096):
-    """Recompute random output windows on the CPU from the L-1 preceding inputs
-    (f64 restatement) and compare: rel-RMS <= 1e-6."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_lib as O
-    worst = 0.0
-    for _ in range(windows):
-        s = int(rng.integers(TAPS, n - width))
-        xs = x_dev_host_fetch(s - (TAPS - 1), s + width)
-        ys = y_dev_host_fetch(s, s + width)
-        ref = O.fir(O.RC64, h.astype(np.float64), 0.2).execute_block(xs.astype(np.complex128))[TAPS - 1:]
-        worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
-    return worst
+# --------------------------------------------------------------------------- workloads
+class Cfg2FIR:
+    """256-tap crcf FIR, firdes_kaiser(256, 0.1, 80) taps rounded to f32, scale 0.2."""
+    metric = "Msamples/sec 256-tap complex FIR @1/2/4/8 GPU; % HBM roofline"
+    taps = 256
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import FIRFilter
+        from solid_dsp_amd.filter import firdes
+        self.n = 1 << args.log2n
+        self.h = firdes.firdes_kaiser(self.taps, 0.1, 80.0, 0.0).astype(np.float32)
+        self.algo = {"fft": sd.ALGO_FFT, "exact": sd.ALGO_EXACT, "fma": sd.ALGO_FMA}[args.algo]
+        self.algo_name = args.algo
+        self.f = FIRFilter(self.h, np.float32(0.2), sample_dtype=np.complex64, device=dev, algo=self.algo)
+        self.make = lambda: FIRFilter(self.h, np.float32(0.2), sample_dtype=np.complex64, device=dev, algo=self.algo)
+        self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        self.d_out = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        self.bytes_per_step = 16 * self.n
+        self.dtype = "c32 (f32 taps x complex-f32 samples, f32 accumulate)"
+        self.kernel = {"fft": "fir_ols4096_kernel (overlap-save N=4096)", "exact": "fir_direct_kernel<EXACT>",
+                       "fma": "fir_direct_kernel<FMA>"}[args.algo]
+        self.workload = (f"cfg2: 256-tap crcf FIR, firdes_kaiser(256, 0.1, 80), scale 0.2, 2^{args.log2n} samples "
+                         "per channel, device resident")
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng, windows=4, width=4096):
+        """random output windows recomputed on the CPU (f64 restatement) from the L-1 preceding inputs"""
+        import oracle_lib as O
+        import torch
+        g = self.make()
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        worst = 0.0
+        L = self.taps
+        for _ in range(windows):
+            s = int(rng.integers(L, self.n - width))
+            xs = self.d_in[s - (L - 1): s + width].cpu().numpy()
+            ys = self.d_out[s: s + width].cpu().numpy()
+            ref = O.fir(O.RC64, self.h.astype(np.float64), 0.2).execute_block(xs.astype(np.complex128))[L - 1:]
+            worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
+        return worst
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = O.synth(SEED, 0, 0, samples, complex_=True).astype(np.complex128)
+        f = O.fir(O.RC64, self.h.astype(np.float64), 0.2)
+        return timed_cpu(lambda: f.execute_block(x), "FIRFilter<f64, Complex<f64>> restatement (memmove Window + "
+                         "to_vec + sequential dot)", samples)
+
+
+class Cfg3IIR:
+    """4-section SOS cascade, scipy butter(8, 0.2), real f32 stream, block-parallel scan."""
+    metric = "Msamples/sec 4-stage IIR biquad cascade (f32, 1 GiS); % HBM roofline"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import IIRFilter, IIRFilterType
+        sos = np.array(json.load(open(os.path.join(REPO, "tests", "golden", "butter8_0p2_sos.json")))["sos"])
+        self.ff = sos[:, :3].reshape(-1).astype(np.float32)
+        self.fb = sos[:, 3:].reshape(-1).astype(np.float32)
+        self.n = 1 << args.log2n
+        self.f = IIRFilter(self.ff, self.fb, IIRFilterType.SecondOrder, sample_dtype=np.float32, device=dev,
+                           algo=sd.ALGO_FMA)
+        self.d_in = torch.empty(self.n, dtype=torch.float32, device="cuda")
+        self.d_out = torch.empty(self.n, dtype=torch.float32, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        self.bytes_per_step = 8 * self.n
+        self.dtype = "f32 (f32 coefficients, real f32 samples)"
+        self.kernel = "sos_scan_kernel<4> (block-parallel scan, warm-up carry)"
+        self.workload = f"cfg3: 4-biquad SOS cascade butter(8, 0.2), real f32, 2^{args.log2n} samples per channel"
+        self.algo_name = "scan"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng):
+        import oracle_lib as O
+        import torch
+        m = 1 << 20  # the first 2^20 outputs of a fresh pass vs the f64 restatement (IIR: full prefix)
+        from solid_dsp_amd import IIRFilter, IIRFilterType
+        import solid_dsp_amd as sd
+        g = IIRFilter(self.ff, self.fb, IIRFilterType.SecondOrder, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        x = self.d_in[:m].cpu().numpy().astype(np.float64)
+        y = self.d_out[:m].cpu().numpy()
+        ref = O.iir(O.RR64, self.ff.astype(np.float64), self.fb.astype(np.float64), O.SECOND_ORDER).execute_block(x)
+        return float(np.linalg.norm(y - ref) / np.linalg.norm(ref))
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = O.synth(SEED, 0, 0, samples).astype(np.float64)
+        f = O.iir(O.RR64, self.ff.astype(np.float64), self.fb.astype(np.float64), O.SECOND_ORDER)
+        return timed_cpu(lambda: f.execute_block(x), "IIRFilter<f64, f64> SecondOrder restatement", samples)
+
+
+class Cfg4Decim:
+    """M=32 decimator, firdes_kaiser(256, 1/64, 80) rounded to f32, scale 1/32, crcf."""
+    metric = "Msamples/sec 32-branch polyphase decimator (M=32, 8 taps/branch); % HBM roofline"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import DecimatingFIRFilter
+        from solid_dsp_amd.filter import firdes
+        self.n = 1 << args.log2n
+        self.h = firdes.firdes_kaiser(256, 1.0 / 64, 80.0, 0.0).astype(np.float32)
+        self.f = DecimatingFIRFilter(self.h, np.float32(1.0 / 32), 32, sample_dtype=np.complex64, device=dev,
+                                     algo=sd.ALGO_FMA)
+        self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        self.d_out = torch.empty(self.n // 32 + 1, dtype=torch.complex64, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        self.bytes_per_step = 8 * self.n + 8 * (self.n // 32)
+        self.dtype = "c32 (f32 taps x complex-f32 samples)"
+        self.kernel = "decim_direct_kernel (reference tap order, fused multiply-add)"
+        self.workload = f"cfg4: M=32 x 8-tap polyphase decimator, crcf, 2^{args.log2n} input samples per channel"
+        self.algo_name = "fma"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng, width=4096):
+        """random windows of outputs recomputed in f64 from the definition
+        y[m] = scale * sum_j h[j] x[32m + 31 - 255 + j]  (fresh handle: first output after input 31)"""
+        import torch
+        from numpy.lib.stride_tricks import sliding_window_view
+        from solid_dsp_amd import DecimatingFIRFilter
+        import solid_dsp_amd as sd
+        g = DecimatingFIRFilter(self.h, np.float32(1.0 / 32), 32, sample_dtype=np.complex64, algo=sd.ALGO_FMA)
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        h = self.h.astype(np.float64)
+        worst = 0.0
+        for _ in range(4):
+            m = int(rng.integers(8, self.n // 32 - width))
+            xs = self.d_in[32 * m - 224: 32 * (m + width)].cpu().numpy().astype(np.complex128)
+            ref = sliding_window_view(xs, 256)[::32][:width] @ h / 32.0
+            ys = self.d_out[m: m + width].cpu().numpy()
+            worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
+        return worst
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = O.synth(SEED, 0, 0, samples, complex_=True).astype(np.complex128)
+        f = O.decim(O.RC64, self.h.astype(np.float64), 1.0 / 32, 32)
+        return timed_cpu(lambda: f.execute_block(x), "DecimatingFIRFilter<f64, Complex<f64>> restatement", samples)
+
+
+class Cfg5Chan:
+    """1024-channel PFB + FFT, prototype firdes_kaiser(8192, 1/2048, 80), 8 streams x 2^24 per GPU."""
+    metric = "Msamples/sec 1024-channel PFB + FFT channeliser (8 streams/GPU); % HBM roofline"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import Channelizer
+        from solid_dsp_amd.filter import firdes
+        self.M, self.S = 1024, 8
+        self.n = 1 << 24
+        self.h = firdes.firdes_kaiser(8192, 1.0 / 2048, 80.0, 0.0).astype(np.float32)
+        self.f = Channelizer(self.h, self.M, sample_dtype=np.complex64, device=dev, streams=self.S)
+        self.d_in = torch.empty(self.S * self.n, dtype=torch.complex64, device="cuda")
+        self.d_out = torch.empty(self.S * self.n, dtype=torch.complex64, device="cuda")
+        from solid_dsp_amd import parallel as P
+        for s, ch in enumerate(P.channel_ids(self.S, 1, rank)):  # streams rank*S .. rank*S+S-1
+            sd.lib().sdsp_synth_f32_device(self.d_in[s * self.n:].data_ptr(), SEED, ch, 0, 2 * self.n,
+                                           torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.S * self.n
+        self.bytes_per_step = 16 * self.S * self.n
+        self.dtype = "c32 (f32 taps x complex-f32 samples)"
+        self.kernel = "chan_kernel (fused PFB + radix-4 Stockham FFT in LDS)"
+        self.workload = "cfg5: 1024-channel PFB (K=8) + 1024-pt FFT, 8 streams x 2^24 samples per GPU"
+        self.algo_name = "chan"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng):
+        import oracle_lib as O
+        import torch
+        from solid_dsp_amd import Channelizer
+        g = Channelizer(self.h, self.M, sample_dtype=np.complex64, streams=self.S)
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        fr = 64  # first 64 frames of stream 0
+        x = self.d_in[: fr * self.M].cpu().numpy().astype(np.complex128)
+        y = self.d_out[: fr * self.M].cpu().numpy()
+        ref = np.zeros(fr * self.M, np.complex128)
+        O.lib().orc_channelize(O._ptr(self.h.astype(np.float64)), len(self.h), self.M, O._ptr(x), len(x), O._ptr(ref))
+        return float(np.linalg.norm(y - ref) / np.linalg.norm(ref))
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        samples = samples // self.M * self.M
+        x = O.synth(SEED, 0, 0, samples, complex_=True).astype(np.complex128)
+        out = np.zeros(samples, np.complex128)
+        h = self.h.astype(np.float64)
+        return timed_cpu(lambda: O.lib().orc_channelize(O._ptr(h), len(h), self.M, O._ptr(x), samples, O._ptr(out)),
+                         "channeliser restatement (PFB DotProducts + reference mixed-radix FFT)", samples)
+
+
+WORKLOADS = {2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan}
+CPU_DEFAULT = {2: 1 << 24, 3: 1 << 24, 4: 1 << 23, 5: 1 << 22}
 
 
 def main():
@@ -92,9 +285,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from solid_dsp_amd import parallel as P
+    rank, world, local = P.world()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -103,27 +295,15 @@ def main():
     dev = torch.cuda.current_device()
 
     import solid_dsp_amd as sd
-    from solid_dsp_amd import FIRFilter
-    from solid_dsp_amd.filter import firdes
-
-    n = 1 << args.log2n
-    h = firdes.firdes_kaiser(TAPS, 0.1, 80.0, 0.0).astype(np.float32)
-    algo = {"fft": sd.ALGO_FFT, "exact": sd.ALGO_EXACT, "fma": sd.ALGO_FMA}[args.algo]
-    f = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, device=dev, algo=algo)
 
     stream = torch.cuda.current_stream()
-    d_in = torch.empty(n, dtype=torch.complex64, device="cuda")
-    d_out = torch.empty(n, dtype=torch.complex64, device="cuda")
-    # synthetic channel `rank` generated on device (untimed)
-    sd.lib().sdsp_synth_f32_device(d_in.data_ptr(), SEED, rank, 0, 2 * n, stream.cuda_stream)
+    w = WORKLOADS[args.config](args, rank, dev, torch, sd)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        f.execute_block_device(d_in, n, d_out, stream)
+        w.step(stream)
     torch.cuda.synchronize()
 
-    # parity on the first warm-up pass is gone (stream state advanced); run a
-    # fresh handle once for the parity windows below
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
@@ -132,50 +312,38 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         starts[k].record(stream)
-        f.execute_block_device(d_in, n, d_out, stream)
+        w.step(stream)
         ends[k].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+    wall = P.max_over_ranks(wall, device="cuda")  # the job runs as long as its slowest rank
 
     # final gather over RCCL (timed separately, not part of `value`): the first
-    # 2^20 outputs of every channel to rank 0
+    # 2^20 outputs of every rank's channel to rank 0
     gather_ms = None
     if world > 1:
-        piece = d_out[: 1 << 20].contiguous()
-        bufs = [torch.empty_like(piece) for _ in range(world)] if rank == 0 else None
+        piece = w.d_out[: 1 << 20].contiguous()
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter()
-        dist.gather(piece, bufs, dst=0)
+        P.gather_to_root(piece, 0)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
     parity = None
     if not args.no_parity and rank == 0:
-        g = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, device=dev, algo=algo)
-        g.execute_block_device(d_in, n, d_out, stream)
-        torch.cuda.synchronize()
-        rng = np.random.default_rng(1)
-        parity = parity_windows(h, lambda a, b: d_in[a:b].cpu().numpy(), lambda a, b: d_out[a:b].cpu().numpy(),
-                                n, rng)
+        parity = w.parity(stream, np.random.default_rng(1))
 
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
-        value = world * n * args.steps / wall / 1e6
+        value = world * w.samples_per_step * args.steps / wall / 1e6
         kern_ms = float(np.mean(ev_ms))
-        achieved = 16.0 * n / (kern_ms * 1e-3) / 1e9  # GB/s of algorithmic traffic (8 B in + 8 B out)
-        tr = load_traffic()
-        traffic = tr["hbm_bytes_per_launch"] if tr and tr.get("log2n") == args.log2n and tr.get("algo") == args.algo \
-            else None
+        achieved = w.bytes_per_step / (kern_ms * 1e-3) / 1e9
         out = {
-            "metric": "Msamples/sec 256-tap complex FIR @1/2/4/8 GPU; % HBM roofline",
+            "metric": w.metric,
             "value": round(value, 1),
             "unit": "Msamples/sec",
             "n_gpus": world,
@@ -185,22 +353,19 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "c32 (f32 taps x complex-f32 samples, f32 accumulate)",
+            "dtype": w.dtype,
             "data": "synthetic SplitMix64 stream (seed 20250226, channel = rank), device generated",
-            "config": {"workload": "cfg2: 256-tap crcf FIR, firdes_kaiser(256, 0.1, 80), scale 0.2, "
-                                   f"2^{args.log2n} samples per channel, device resident",
-                       "samples_per_step_per_gpu": n, "taps": TAPS,
-                       "kernel": {"fft": "fir_ols4096_kernel (overlap-save N=4096)",
-                                  "exact": "fir_direct_kernel<EXACT>", "fma": "fir_direct_kernel<FMA>"}[args.algo],
-                       "parallelism": f"channels sharded, 1 per GPU x {world}"},
+            "config": {"workload": w.workload, "samples_per_step_per_gpu": w.samples_per_step,
+                       "kernel": w.kernel, "parallelism": f"channels sharded, independent per GPU x {world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": 16 * n},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(args.config, args.log2n, w.algo_name),
+                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": w.bytes_per_step},
             "parity_rel_rms_vs_f64_oracle": parity,
             "gather_ms": gather_ms,
         }
         if not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(h, args.cpu_samples)
+            out["cpu_baseline"] = w.cpu(args.cpu_samples or CPU_DEFAULT[args.config])
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

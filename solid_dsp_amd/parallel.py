@@ -1,0 +1,53 @@
+"""Multi-GPU harness for the engine: one process per GPU,
+independent channels/streams sharded across ranks with no data-path
+collective, max-over-ranks timing, and an RCCL gather of results to rank 0
+after the timed region.
+
+Backend-agnostic on purpose: bench.py runs it over RCCL ("nccl") with device
+tensors; tests/test_parallel_gloo.py runs the same functions over gloo with
+CPU tensors at world size 2.
+"""
+from __future__ import annotations
+
+import os
+
+
+def world():
+    """(rank, world_size, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard(total: int, world_size: int, rank: int) -> list[int]:
+    """Round-robin shard of `total` independent channels: rank r gets r, r+W, r+2W, ..."""
+    if world_size < 1 or not (0 <= rank < world_size):
+        raise ValueError("bad rank / world size")
+    return list(range(rank, total, world_size))
+
+
+def channel_ids(per_rank: int, world_size: int, rank: int) -> list[int]:
+    """Weak scaling: every rank owns `per_rank` channels; global ids rank*per_rank + s."""
+    return [rank * per_rank + s for s in range(per_rank)]
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """The job's time is the slowest rank's (all_reduce MAX)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_to_root(piece, root: int = 0):
+    """Gather one equally-shaped tensor per rank onto `root` (list on root, None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [piece]
+    rank = dist.get_rank()
+    bufs = [torch.empty_like(piece) for _ in range(dist.get_world_size())] if rank == root else None
+    dist.gather(piece.contiguous(), bufs, dst=root)
+    return bufs
