@@ -121,7 +121,8 @@ typedef enum {
     SDSP_TUNE_OLS_INTERLEAVE = 2,
     SDSP_TUNE_OLS_DEPTH2 = 3,
     SDSP_TUNE_OLS_ABLATE_NOMEM = 4,
-    SDSP_TUNE_OLS_OCCUPANCY = 5 /* 0 = 2-wave kernel, 3/4 = single-region kernel at 3/4 blocks per CU */
+    SDSP_TUNE_OLS_OCCUPANCY = 5, /* 0 = 2-wave kernel, 3/4 = single-region kernel at 3/4 blocks per CU */
+    SDSP_TUNE_DECIM_SEG = 6      /* FMA decimator: outputs per lane group (0 = automatic) */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */

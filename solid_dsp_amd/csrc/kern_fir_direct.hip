@@ -288,6 +288,8 @@ hipError_t launch_fir_direct(int dtype, const FirArgs& a, hipStream_t s) {
 }
 hipError_t launch_decim_direct(int dtype, const FirArgs& a, hipStream_t s) {
     if (a.nout == 0) return hipSuccess;
+    hipError_t err;
+    if (try_launch_decim_poly(dtype, a, s, &err)) return err;
     SDSP_DISPATCH_DTYPE(dtype, launch_decim_direct_t, a, s)
 }
 hipError_t launch_hist_update(int dtype, const void* x, const void* old_hist, void* new_hist, size_t n, int Lm1,

@@ -99,6 +99,7 @@ struct sdsp_fir {
     bool ols_ok = false;
     bool ols_wide = false, ols_interleave = true, ols_depth2 = false, ols_nomem = false;
     int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
+    int decim_seg = 0;  // outputs per lane group of the polyphase decimator (0 = auto)
     OlsPlan ols{};
     DevBuf d_H, d_tw1, d_tw2;
 };
@@ -312,6 +313,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
         case SDSP_TUNE_OLS_DEPTH2: h->ols_depth2 = value != 0; break;
         case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = value != 0; break;
         case SDSP_TUNE_OLS_OCCUPANCY: h->ols_occ = (value == 3 || value == 4) ? value : 0; break;
+        case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }
     h->ols.wide = h->ols_wide;
@@ -397,6 +399,7 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
         const int algo = h->algo == SDSP_ALGO_FMA ? SDSP_ALGO_FMA : SDSP_ALGO_EXACT;
         FirArgs a{d_in, hist, h->d_taps_rev.p, h->scale.data(), d_out, n, nout, h->channels, (int)h->L, (int)h->M,
                   j0, algo != SDSP_ALGO_FMA};
+        a.seg = h->decim_seg;
         SDSP_TRY(launch_decim_direct(h->dtype, a, s), "decim direct");
         h->ci = (h->ci + n) % h->M;
     }

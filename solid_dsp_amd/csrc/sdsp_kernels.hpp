@@ -17,10 +17,13 @@ struct FirArgs {
     int L, M;
     size_t j0;             // block-relative index of the first emitting input (decimator)
     bool exact;
+    int seg = 0;           // polyphase decimator: outputs per lane group (0 = auto)
 };
 
 hipError_t launch_fir_direct(int dtype, const FirArgs& a, hipStream_t s);
 hipError_t launch_decim_direct(int dtype, const FirArgs& a, hipStream_t s);
+// column-parallel polyphase decimator (kern_decim.hip); false = not applicable
+bool try_launch_decim_poly(int dtype, const FirArgs& a, hipStream_t s, hipError_t* err);
 hipError_t launch_hist_update(int dtype, const void* x, const void* old_hist, void* new_hist, size_t n, int Lm1,
                               size_t channels, hipStream_t s);
 

@@ -189,6 +189,49 @@ def test_decim_exact_bit_parity(dt, cdt, sdt, L, M):
     assert bits_equal(d.execute_block(x[:500]), o.execute_block(x[:500]))
 
 
+def _wide(dt):
+    return {O.RR32: O.RR64, O.RC32: O.RC64, O.CC32: O.CC64}.get(dt, dt)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", DTYPES)
+@pytest.mark.parametrize("L,M", [(256, 32), (128, 16), (64, 8), (512, 64), (32, 16), (1024, 64), (300, 7)])
+def test_decim_fma_tolerance(dt, cdt, sdt, L, M):
+    # column-parallel polyphase kernel (L = K*M, K in {2,4,8,16}) or the tiled fallback;
+    # streaming over ragged calls with push/write phase moves, vs the f64 restatement
+    rng = np.random.default_rng(L * 3 + M + dt)
+    h = rand(rng, L, cdt)
+    x = rand(rng, 200000, sdt)
+    d = DecimatingFIRFilter(h, cdt(0.5), M, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    w = _wide(dt)
+    wide = {O.RR64: F64, O.RC64: F64, O.CC64: C128}[w]
+    o = O.decim(w, h.astype(wide), wide(0.5), M)
+    xw = x.astype(C128 if np.dtype(sdt).kind == "c" else F64)
+    tol = 1e-6 if np.dtype(sdt).itemsize <= 8 and sdt != F64 else 1e-13
+    ys, yos = [], []
+    for a, b in [(0, 1), (1, 2), (2, 35), (35, 35), (35, 17000), (17000, 150001), (150001, 200000)]:
+        ys.append(d.execute_block(x[a:b]))
+        yos.append(o.execute_block(xw[a:b]))
+    assert rel_rms(np.concatenate(ys), np.concatenate(yos)) <= tol
+    d.push(x[0]); o.push(xw[0])
+    d.write(x[:13]); o.write(xw[:13])
+    assert rel_rms(d.execute_block(x[:50000]), o.execute_block(xw[:50000])) <= tol
+
+
+def test_decim_fma_multichannel_device():
+    import torch
+    h = O.firdes_kaiser(256, 1.0 / 64, 80.0, 0.0).astype(F32)
+    ch, n = 3, 1 << 20
+    x = np.stack([O.synth(2, c, 0, n, complex_=True) for c in range(ch)])
+    d = DecimatingFIRFilter(h, F32(1.0 / 32), 32, sample_dtype=C64, channels=ch, algo=sd.ALGO_FMA)
+    d_in = to_dev(x.reshape(-1))
+    d_out = empty_dev(ch * (n // 32), C64)
+    assert d.execute_block_device(d_in, n, d_out, torch.cuda.current_stream()) == n // 32
+    y = to_host(d_out).reshape(ch, n // 32)
+    for c in range(ch):
+        ref = O.decim(O.RC64, h.astype(F64), 1.0 / 32, 32).execute_block(x[c].astype(C128))
+        assert rel_rms(y[c], ref) <= 1e-6
+
+
 def test_decim_cfg4_shape():
     # cfg4: 32 branches x 8 taps, M = 32, crcf
     h = O.firdes_kaiser(256, 1.0 / 64, 80.0, 0.0).astype(F32)

@@ -61,6 +61,46 @@ __global__ void __launch_bounds__(256) write_k(float4* __restrict__ b, long long
     }
 }
 
+// one-shot read: every thread U float4s, grid covers the buffer
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) read_once_k(const float4* __restrict__ a_, float* __restrict__ out, long long n16) {
+    const f4v* a = reinterpret_cast<const f4v*>(a_);
+    const long long base = (long long)blockIdx.x * 256 * U + threadIdx.x;
+    f4v s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+        const long long i = base + 256 * k;
+        if (i < n16) {
+            if constexpr (NT) s += __builtin_nontemporal_load(a + i);
+            else s += a[i];
+        }
+    }
+    if (s.x + s.y + s.z + s.w == 12345.f) out[blockIdx.x] = s.x;
+}
+
+// decimator-like: 16-lane groups each stream 256-byte rows through their own
+// segment of SEG bytes, 8 rows per step
+template <bool NT>
+__global__ void __launch_bounds__(256) read_seg_k(const float4* __restrict__ a_, float* __restrict__ out, long long n16,
+                                                  long long seg16) {
+    const f4v* a = reinterpret_cast<const f4v*>(a_);
+    const long long grp = ((long long)blockIdx.x * 256 + threadIdx.x) / 16;
+    const int q = threadIdx.x % 16;
+    const long long b0 = grp * seg16;
+    f4v s = {0.f, 0.f, 0.f, 0.f};
+    if (b0 < n16) {
+        for (long long r = 0; r < seg16; r += 16 * 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const long long i = b0 + r + u * 16 + q;
+                if constexpr (NT) s += __builtin_nontemporal_load(a + i);
+                else s += a[i];
+            }
+        }
+    }
+    if (s.x + s.y + s.z + s.w == 12345.f) out[blockIdx.x] = s.x;
+}
+
 template <typename F>
 float time_ms(F f, int reps = 10) {
     hipEvent_t e0, e1;
@@ -110,6 +150,25 @@ int main() {
         rep(nm, time_ms([&] { read_k<8><<<cus * g, 256>>>(a, out, n16); }), 1.0 * bytes);
         std::snprintf(nm, 64, "write U8 grid=%dxCU", g);
         rep(nm, time_ms([&] { write_k<8><<<cus * g, 256>>>(b, n16); }), 1.0 * bytes);
+    }
+    for (int u : {1, 4}) {
+        char nm[64];
+        const long long per = 256LL * u;
+        const unsigned gb = (unsigned)((n16 + per - 1) / per);
+        std::snprintf(nm, 64, "read one-shot U%d", u);
+        rep(nm, time_ms([&] { if (u == 1) read_once_k<1, false><<<gb, 256>>>(a, out, n16); else read_once_k<4, false><<<gb, 256>>>(a, out, n16); }), 1.0 * bytes);
+        std::snprintf(nm, 64, "read one-shot U%d nt", u);
+        rep(nm, time_ms([&] { if (u == 1) read_once_k<1, true><<<gb, 256>>>(a, out, n16); else read_once_k<4, true><<<gb, 256>>>(a, out, n16); }), 1.0 * bytes);
+    }
+    for (long long segb : {4096LL, 16384LL, 65536LL, 262144LL}) {
+        char nm[64];
+        const long long seg16 = segb / 16;
+        const long long groups = n16 / seg16;
+        const unsigned gb = (unsigned)((groups * 16 + 255) / 256);
+        std::snprintf(nm, 64, "read segmented %lldB", segb);
+        rep(nm, time_ms([&] { read_seg_k<false><<<gb, 256>>>(a, out, n16, seg16); }), 1.0 * bytes);
+        std::snprintf(nm, 64, "read segmented %lldB nt", segb);
+        rep(nm, time_ms([&] { read_seg_k<true><<<gb, 256>>>(a, out, n16, seg16); }), 1.0 * bytes);
     }
     rep("copy U1 one-shot grid", time_ms([&] { copy_k<1, false><<<(unsigned)(n16 / 256), 256>>>(a, b, n16); }),
         2.0 * bytes);
