@@ -122,7 +122,9 @@ typedef enum {
     SDSP_TUNE_OLS_DEPTH2 = 3,
     SDSP_TUNE_OLS_ABLATE_NOMEM = 4,
     SDSP_TUNE_OLS_OCCUPANCY = 5, /* 0 = 2-wave kernel, 3/4 = single-region kernel at 3/4 blocks per CU */
-    SDSP_TUNE_DECIM_SEG = 6      /* FMA decimator: outputs per lane group (0 = automatic) */
+    SDSP_TUNE_DECIM_SEG = 6,     /* FMA decimator: outputs per lane group (0 = automatic) */
+    SDSP_TUNE_IIR_WAVE_SCAN = 7  /* IIR scan kernel: 0 = block scan, 1 (default) = wave scan with 256-byte chunks,
+                                    2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */
@@ -224,6 +226,8 @@ SDSP_API void sdsp_iir_destroy(sdsp_iir* h);
 SDSP_API int sdsp_iir_clone(const sdsp_iir* h, sdsp_iir** out);
 SDSP_API int sdsp_iir_set_channels(sdsp_iir* h, size_t channels);
 SDSP_API int sdsp_iir_set_algo(sdsp_iir* h, int algo);
+/* kernel-variant knob (SDSP_TUNE_IIR_WAVE_SCAN; performance only) */
+SDSP_API int sdsp_iir_set_tuning(sdsp_iir* h, int key, int value);
 /* scan plan of section group g: warm-up chunks (0 = scan not admissible) and chunk length */
 SDSP_API int sdsp_iir_scan_info(const sdsp_iir* h, int group, int* warmup_chunks, int* chunk);
 SDSP_API size_t sdsp_iir_output_count(const sdsp_iir* h, size_t n);

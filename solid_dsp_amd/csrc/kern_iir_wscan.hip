@@ -1,0 +1,651 @@
+// Wave-level block-parallel scan for SOS cascades (gfx950), SDSP_ALGO_FMA /
+// AUTO path of IIRFilter SecondOrder (src/filter/iir/sos.rs:92-114,
+// mod.rs:270-289) when the handle neither decimates nor interpolates.
+//
+// The cascade is linear in its D = 2S state:  S[n+1] = A S[n] + b x[n],
+// y[n] = c S[n] + d x[n].  Each wave walks its own segment of the stream as a
+// sequence of tiles of 64 chunks x B samples (one chunk per lane), with no
+// block barriers:
+//   1. the tile is staged in the wave's LDS slab with coalesced 16-byte
+//      nontemporal loads, one padded row per chunk;
+//   2. lane l runs its row from zero state, writing y0 back in place, and
+//      keeps its local final state s_l;
+//   3. the exact state entering the tile (`carry`, wave-uniform) is folded in
+//      at lane 0: s_0 += A^B carry; a Hillis-Steele scan across the 64 lanes
+//      with P_k = A^(B 2^k) gives every lane the true state at the end of its
+//      chunk, G_l; the initial state of chunk l is I_l = G_{l-1} (I_0 = carry)
+//      and the next tile's carry is G_63.  A and its powers are lower block
+//      triangular (section q depends on sections <= q), so only those blocks
+//      are multiplied;
+//   4. outputs are corrected instead of rerun:  y[i] = y0[i] + Cr[i] . I_l,
+//      Cr[i] = c A^i (the output response to the state, precomputed on the
+//      host in f64), then leave with coalesced nontemporal 16-byte stores.
+// A wave's first tile starts `wc` chunks before its segment: those lanes run
+// the preceding input as warm-up (outputs dropped), which makes the carried-in
+// state exact to ||A^(wc B)|| < 1e-9 (f32) / 1e-17 (f64), the criterion the
+// host applies before it selects any scan.  Wave 0 instead injects the call's
+// exact carried state at lane wc-1 of its first tile.  The lane holding the
+// call's last sample reruns its chunk from I_l and writes the exact final
+// state for the next call.
+#include "sdsp_device.hpp"
+#include "sdsp_kernels.hpp"
+
+#include <type_traits>
+
+namespace sdsp {
+
+namespace {
+
+constexpr int kWsThreads = 256;
+constexpr int kWsWaves = kWsThreads / 64;
+
+// chunk of CB bytes per lane (B = CB / sizeof(I) samples); LDS rows padded by
+// 16 bytes so that 16 lanes reading the same slot of their rows are conflict-free
+template <int CB> struct WsGeom {
+    static constexpr int kRowBytes = CB + 16;
+    static constexpr int kVecPerRow = CB / 16;
+    static constexpr int kSlabBytes = 64 * kRowBytes;  // one tile per wave
+};
+template <typename I, int CB> struct ws_chunk { static constexpr int B = CB / (int)sizeof(I); };
+
+template <typename T> __device__ __forceinline__ T shfl_up_v(T v, int d) { return __shfl_up(v, d); }
+template <typename T> __device__ __forceinline__ cpx<T> shfl_up_v(cpx<T> v, int d) {
+    return {__shfl_up(v.re, d), __shfl_up(v.im, d)};
+}
+template <typename T> __device__ __forceinline__ T readlane_v(T v, int l) { return __shfl(v, l); }
+template <typename T> __device__ __forceinline__ cpx<T> readlane_v(cpx<T> v, int l) {
+    return {__shfl(v.re, l), __shfl(v.im, l)};
+}
+
+// LDS hand-off between the lanes of one wave: wait for this wave's LDS
+// operations only (lgkmcnt(0); vmcnt/expcnt left at their maxima so that
+// in-flight global loads and stores keep running), and keep the compiler from
+// moving memory operations across
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+}
+
+// one cascade step, fused form: w = x - a1 w1 - a2 w2;  y = b0 w + b1 w1 + b2 w2
+template <int S, typename C, typename I>
+__device__ __forceinline__ I sos_step_f(const C* __restrict__ c, I v, I (&w1)[S], I (&w2)[S]) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const I w = fmac_(fmac_(v, -c[5 * s + 4], w2[s]), -c[5 * s + 3], w1[s]);
+        v = fmac_(fmac_(mul_(c[5 * s + 2], w2[s]), c[5 * s + 1], w1[s]), c[5 * s + 0], w);
+        w2[s] = w1[s];
+        w1[s] = w;
+    }
+    return v;
+}
+
+// y = P x for a lower block-triangular P (2x2 blocks), wave-uniform
+template <int D, typename C, typename I>
+__device__ __forceinline__ void matvec_lt(const C* __restrict__ P, const I (&x)[D], I (&y)[D]) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const int cmax = (r / 2) * 2 + 2;
+        I acc = mul_(P[r * D], x[0]);
+#pragma unroll
+        for (int c = 1; c < cmax; ++c) acc = fmac_(acc, P[r * D + c], x[c]);
+        y[r] = acc;
+    }
+}
+
+using v4u = unsigned __attribute__((ext_vector_type(4)));
+
+template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / sizeof(I)]) {
+    v4u v;
+    __builtin_memcpy(&v, e, 16);
+    return v;
+}
+
+template <int S, typename C, typename I, int CB>
+__global__ void __launch_bounds__(kWsThreads)
+sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
+                 const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
+                 const I* __restrict__ st_in, I* __restrict__ st_out, long long nd, int wc, int tpw, bool vec_ok) {
+    constexpr int D = 2 * S;
+    constexpr int B = ws_chunk<I, CB>::B;
+    constexpr int E = 16 / (int)sizeof(I);  // samples per 16-byte vector
+    constexpr int kRowBytes = WsGeom<CB>::kRowBytes, kVecPerRow = WsGeom<CB>::kVecPerRow;
+    constexpr int kSlabBytes = WsGeom<CB>::kSlabBytes;
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    char* slab = lds_raw + wave * kSlabBytes;
+    char* row = slab + lane * kRowBytes;
+    C* sP = reinterpret_cast<C*>(lds_raw + kWsWaves * kSlabBytes);
+    C* sCr = sP + 6 * D * D;
+    for (int i = threadIdx.x; i < 6 * D * D; i += kWsThreads) sP[i] = P[i];
+    for (int i = threadIdx.x; i < B * D; i += kWsThreads) sCr[i] = Cr[i];
+    __syncthreads();
+
+    const int ch = blockIdx.y;
+    x += (long long)ch * nd;
+    y += (long long)ch * nd;
+    st_in += (long long)ch * D;
+    st_out += (long long)ch * D;
+
+    const long long gw = (long long)blockIdx.x * kWsWaves + wave;  // wave's segment
+    const long long segc = (long long)tpw * 64 - wc;                  // chunks per segment
+    const long long c_lo = gw * segc;                                 // first chunk of the segment
+    const long long k_lo = c_lo * B;
+    if (k_lo >= nd) return;
+
+    I carry[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) carry[d] = zero_v<I>();
+
+    // interior tiles are read with straight-line 16-byte loads, one tile ahead of
+    // the compute (a per-vector branch would serialise the HBM round trips)
+    auto interior_at = [&](long long k0) { return vec_ok && k0 >= 0 && k0 + 64LL * B <= nd; };
+    v4u pre[kVecPerRow];
+    {
+        const long long k0 = (c_lo - wc) * B;
+        if (interior_at(k0)) {
+#pragma unroll
+            for (int j = 0; j < kVecPerRow; ++j)
+                pre[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + k0) + lane + 64 * j);
+        }
+    }
+
+    for (int t = 0; t < tpw; ++t) {
+        const long long k0 = (c_lo - wc + (long long)t * 64) * B;  // first sample of the tile
+        if (k0 >= nd) break;
+
+        // 1. stage the tile: vector v of the tile -> row v / kVecPerRow, slot v % kVecPerRow
+        const bool interior = interior_at(k0);
+        if (interior) {
+#pragma unroll
+            for (int j = 0; j < kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                *reinterpret_cast<v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16) = pre[j];
+            }
+        } else {
+            for (int j = 0; j < kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                const long long kv = k0 + (long long)v * E;
+                I tmp[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) tmp[e] = (kv + e >= 0 && kv + e < nd) ? x[kv + e] : zero_v<I>();
+                *reinterpret_cast<v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16) = to_v4<I>(tmp);
+            }
+        }
+        {  // prefetch the next tile (whatever path this one took)
+            const long long kn = k0 + 64LL * B;
+            if (t + 1 < tpw && interior_at(kn)) {
+#pragma unroll
+                for (int j = 0; j < kVecPerRow; ++j)
+                    pre[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + kn) + lane + 64 * j);
+            }
+        }
+        wave_sync();
+
+        // 2. zero-state run over my row, y0 in place
+        I s[D];
+        {
+            I w1[S], w2[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) { w1[q] = zero_v<I>(); w2[q] = zero_v<I>(); }
+#pragma unroll 2
+            for (int o = 0; o < kVecPerRow; ++o) {
+                I e[E];
+                const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
+                __builtin_memcpy(e, &val, 16);
+#pragma unroll
+                for (int i = 0; i < E; ++i) e[i] = sos_step_f<S>(coefs, e[i], w1, w2);
+                *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
+            }
+#pragma unroll
+            for (int q = 0; q < S; ++q) { s[2 * q] = w1[q]; s[2 * q + 1] = w2[q]; }
+        }
+        if (gw == 0 && t == 0 && lane == wc - 1) {  // the call's exact carried state enters here
+#pragma unroll
+            for (int d = 0; d < D; ++d) s[d] = st_in[d];
+        }
+        // 3. fold the carry into lane 0, then the inclusive scan over lanes
+        {
+            I a[D];
+            matvec_lt<D>(sP, carry, a);
+            if (lane == 0) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) s[d] = add_(s[d], a[d]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int off = 1 << k;
+            I prev[D], a[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) prev[d] = shfl_up_v(s[d], off);
+            matvec_lt<D>(sP + k * D * D, prev, a);
+            if (lane >= off) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) s[d] = add_(s[d], a[d]);
+            }
+        }
+        I init[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const I up = shfl_up_v(s[d], 1);
+            init[d] = lane == 0 ? carry[d] : up;
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) carry[d] = readlane_v(s[d], 63);
+
+        // 4. correction by the state response
+#pragma unroll 2
+        for (int o = 0; o < kVecPerRow; ++o) {
+            I e[E];
+            const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
+            __builtin_memcpy(e, &val, 16);
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                const C* cr = sCr + (o * E + i) * D;
+#pragma unroll
+                for (int d = 0; d < D; ++d) e[i] = fmac_(e[i], cr[d], init[d]);
+            }
+            *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
+        }
+
+        // exact final state: the lane of this segment holding sample nd-1 reruns its chunk
+        const long long kc = k0 + (long long)lane * B;
+        if (kc >= k_lo && kc <= nd - 1 && nd - 1 < kc + B) {
+            I w1[S], w2[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) { w1[q] = init[2 * q]; w2[q] = init[2 * q + 1]; }
+            for (long long k = kc; k < nd; ++k) (void)sos_step_f<S>(coefs, x[k], w1, w2);
+#pragma unroll
+            for (int q = 0; q < S; ++q) { st_out[2 * q] = w1[q]; st_out[2 * q + 1] = w2[q]; }
+        }
+        wave_sync();
+
+        // 5. coalesced store of the segment's samples
+        if (interior && k0 >= k_lo) {
+#pragma unroll
+            for (int j = 0; j < kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                const v4u val = *reinterpret_cast<const v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16);
+                __builtin_nontemporal_store(val, reinterpret_cast<v4u*>(y + k0) + v);
+            }
+        } else {
+            for (int j = 0; j < kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                const long long kv = k0 + (long long)v * E;
+                const v4u val =
+                    *reinterpret_cast<const v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16);
+                I tmp[E];
+                __builtin_memcpy(tmp, &val, 16);
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (kv + e >= k_lo && kv + e < nd) y[kv + e] = tmp[e];
+            }
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------- paired chunks (real f32)
+// Same algorithm with two chunks per lane: lane l owns virtual lanes l and
+// 64 + l of a 128-chunk tile, so the recurrence, the scan's matrix products and
+// the correction run as packed (v_pk_fma_f32) pairs.  The scan spans 128
+// virtual lanes: shifts below 64 take the high half's predecessor from the
+// low half of lane l - d + 64; the shift by 64 is the lane's own low half.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 splat(float c) { return f2{c, c}; }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <int S>
+__device__ __forceinline__ f2 sos_step_p(const float* __restrict__ c, f2 v, f2 (&w1)[S], f2 (&w2)[S]) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const f2 w = pfma(splat(-c[5 * s + 3]), w1[s], pfma(splat(-c[5 * s + 4]), w2[s], v));
+        v = pfma(splat(c[5 * s + 0]), w, pfma(splat(c[5 * s + 1]), w1[s], splat(c[5 * s + 2]) * w2[s]));
+        w2[s] = w1[s];
+        w1[s] = w;
+    }
+    return v;
+}
+
+template <int D>
+__device__ __forceinline__ void matvec_lt_p(const float* __restrict__ P, const f2 (&x)[D], f2 (&y)[D]) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const int cmax = (r / 2) * 2 + 2;
+        f2 acc = splat(P[r * D]) * x[0];
+#pragma unroll
+        for (int c = 1; c < cmax; ++c) acc = pfma(splat(P[r * D + c]), x[c], acc);
+        y[r] = acc;
+    }
+}
+
+template <int S, int CB>
+__global__ void __launch_bounds__(kWsThreads)
+sos_wscan2_kernel(const float* __restrict__ x, float* __restrict__ y, const float* __restrict__ coefs,
+                  const float* __restrict__ P /* [7][D][D] */, const float* __restrict__ Cr /* [B][D] */,
+                  const float* __restrict__ st_in, float* __restrict__ st_out, long long nd, int wc, int tpw,
+                  bool vec_ok) {
+    constexpr int D = 2 * S;
+    constexpr int B = CB / 4;
+    constexpr int E = 4;
+    constexpr int kRowBytes = CB + 16, kVecPerRow = CB / 16;
+    constexpr int kSlabBytes = 128 * kRowBytes;
+    constexpr int TC = 128;  // chunks per tile
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    char* slab = lds_raw + wave * kSlabBytes;
+    char* row_a = slab + lane * kRowBytes;
+    char* row_b = slab + (64 + lane) * kRowBytes;
+    float* sP = reinterpret_cast<float*>(lds_raw + kWsWaves * kSlabBytes);
+    float* sCr = sP + 7 * D * D;
+    for (int i = threadIdx.x; i < 7 * D * D; i += kWsThreads) sP[i] = P[i];
+    for (int i = threadIdx.x; i < B * D; i += kWsThreads) sCr[i] = Cr[i];
+    __syncthreads();
+
+    const int ch = blockIdx.y;
+    x += (long long)ch * nd;
+    y += (long long)ch * nd;
+    st_in += (long long)ch * D;
+    st_out += (long long)ch * D;
+
+    const long long gw = (long long)blockIdx.x * kWsWaves + wave;
+    const long long segc = (long long)tpw * TC - wc;
+    const long long c_lo = gw * segc;
+    const long long k_lo = c_lo * B;
+    if (k_lo >= nd) return;
+
+    float carry[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) carry[d] = 0.0f;
+
+    for (int t = 0; t < tpw; ++t) {
+        const long long k0 = (c_lo - wc + (long long)t * TC) * B;
+        if (k0 >= nd) break;
+
+        const bool interior = vec_ok && k0 >= 0 && k0 + (long long)TC * B <= nd;
+        if (interior) {
+            v4u val[2 * kVecPerRow];
+#pragma unroll
+            for (int j = 0; j < 2 * kVecPerRow; ++j)
+                val[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + k0) + lane + 64 * j);
+#pragma unroll
+            for (int j = 0; j < 2 * kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                *reinterpret_cast<v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16) = val[j];
+            }
+        } else {
+            for (int j = 0; j < 2 * kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                const long long kv = k0 + (long long)v * E;
+                float tmp[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) tmp[e] = (kv + e >= 0 && kv + e < nd) ? x[kv + e] : 0.0f;
+                v4u val;
+                __builtin_memcpy(&val, tmp, 16);
+                *reinterpret_cast<v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16) = val;
+            }
+        }
+        wave_sync();
+
+        // zero-state run of both chunks, packed
+        f2 s[D];
+        {
+            f2 w1[S], w2[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) { w1[q] = splat(0.0f); w2[q] = splat(0.0f); }
+#pragma unroll 2
+            for (int o = 0; o < kVecPerRow; ++o) {
+                float ea[E], eb[E];
+                const v4u va = *reinterpret_cast<const v4u*>(row_a + o * 16);
+                const v4u vb = *reinterpret_cast<const v4u*>(row_b + o * 16);
+                __builtin_memcpy(ea, &va, 16);
+                __builtin_memcpy(eb, &vb, 16);
+#pragma unroll
+                for (int i = 0; i < E; ++i) {
+                    const f2 r = sos_step_p<S>(coefs, f2{ea[i], eb[i]}, w1, w2);
+                    ea[i] = r.x;
+                    eb[i] = r.y;
+                }
+                v4u oa, ob;
+                __builtin_memcpy(&oa, ea, 16);
+                __builtin_memcpy(&ob, eb, 16);
+                *reinterpret_cast<v4u*>(row_a + o * 16) = oa;
+                *reinterpret_cast<v4u*>(row_b + o * 16) = ob;
+            }
+#pragma unroll
+            for (int q = 0; q < S; ++q) { s[2 * q] = w1[q]; s[2 * q + 1] = w2[q]; }
+        }
+        if (gw == 0 && t == 0) {  // the call's exact carried state enters at virtual lane wc-1
+            const int vl = wc - 1;
+            if (vl < 64 && lane == vl) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) s[d].x = st_in[d];
+            } else if (vl >= 64 && lane == vl - 64) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) s[d].y = st_in[d];
+            }
+        }
+        // carry into virtual lane 0
+        {
+            f2 cin[D], a[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) cin[d] = splat(carry[d]);
+            matvec_lt_p<D>(sP, cin, a);
+            if (lane == 0) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) s[d].x += a[d].x;
+            }
+        }
+        // inclusive scan over 128 virtual lanes
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int off = 1 << k;
+            const int src = (lane - off) & 63;
+            const bool in = lane >= off;
+            f2 prev[D], a[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const float pa = __shfl(s[d].x, src);
+                const float pb = __shfl(s[d].y, src);
+                prev[d] = f2{pa, in ? pb : pa};
+            }
+            matvec_lt_p<D>(sP + k * D * D, prev, a);
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                if (in) s[d].x += a[d].x;
+                s[d].y += a[d].y;
+            }
+        }
+        {  // shift by 64: high half += A^(64B) * own low half
+            float lo[D], a[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) lo[d] = s[d].x;
+            matvec_lt<D>(sP + 6 * D * D, lo, a);
+#pragma unroll
+            for (int d = 0; d < D; ++d) s[d].y += a[d];
+        }
+        f2 init[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float ua = __shfl(s[d].x, (lane - 1) & 63);  // lane 0 reads lane 63's low half
+            const float ub = __shfl(s[d].y, (lane - 1) & 63);
+            init[d] = f2{lane == 0 ? carry[d] : ua, lane == 0 ? ua : ub};
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) carry[d] = __shfl(s[d].y, 63);
+
+        // correction, packed
+#pragma unroll 2
+        for (int o = 0; o < kVecPerRow; ++o) {
+            float ea[E], eb[E];
+            const v4u va = *reinterpret_cast<const v4u*>(row_a + o * 16);
+            const v4u vb = *reinterpret_cast<const v4u*>(row_b + o * 16);
+            __builtin_memcpy(ea, &va, 16);
+            __builtin_memcpy(eb, &vb, 16);
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                const float* cr = sCr + (o * E + i) * D;
+                f2 acc = f2{ea[i], eb[i]};
+#pragma unroll
+                for (int d = 0; d < D; ++d) acc = pfma(splat(cr[d]), init[d], acc);
+                ea[i] = acc.x;
+                eb[i] = acc.y;
+            }
+            v4u oa, ob;
+            __builtin_memcpy(&oa, ea, 16);
+            __builtin_memcpy(&ob, eb, 16);
+            *reinterpret_cast<v4u*>(row_a + o * 16) = oa;
+            *reinterpret_cast<v4u*>(row_b + o * 16) = ob;
+        }
+
+        // exact final state from the virtual lane of this segment holding sample nd-1
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const long long kc = k0 + (long long)(lane + 64 * h) * B;
+            if (kc >= k_lo && kc <= nd - 1 && nd - 1 < kc + B) {
+                float w1[S], w2[S];
+#pragma unroll
+                for (int q = 0; q < S; ++q) {
+                    w1[q] = h ? init[2 * q].y : init[2 * q].x;
+                    w2[q] = h ? init[2 * q + 1].y : init[2 * q + 1].x;
+                }
+                for (long long k = kc; k < nd; ++k) (void)sos_step_f<S>(coefs, x[k], w1, w2);
+#pragma unroll
+                for (int q = 0; q < S; ++q) { st_out[2 * q] = w1[q]; st_out[2 * q + 1] = w2[q]; }
+            }
+        }
+        wave_sync();
+
+        if (interior && k0 >= k_lo) {
+#pragma unroll
+            for (int j = 0; j < 2 * kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                const v4u val = *reinterpret_cast<const v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16);
+                __builtin_nontemporal_store(val, reinterpret_cast<v4u*>(y + k0) + v);
+            }
+        } else {
+            for (int j = 0; j < 2 * kVecPerRow; ++j) {
+                const int v = lane + 64 * j;
+                const long long kv = k0 + (long long)v * E;
+                const v4u val =
+                    *reinterpret_cast<const v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16);
+                float tmp[E];
+                __builtin_memcpy(tmp, &val, 16);
+#pragma unroll
+                for (int e = 0; e < E; ++e)
+                    if (kv + e >= k_lo && kv + e < nd) y[kv + e] = tmp[e];
+            }
+        }
+        wave_sync();
+    }
+}
+
+template <int S, int CB>
+hipError_t launch_wscan2_t(const IirArgs& a, hipStream_t st) {
+    constexpr int B = CB / 4;
+    const long long nd = (long long)a.n;
+    const long long nch = (nd + B - 1) / B;
+    int tpw = (int)(nch / (128LL * 4096));
+    tpw = tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
+    const long long segc = (long long)tpw * 128 - a.wc;
+    const long long waves = (nch + segc - 1) / segc;
+    dim3 grid((unsigned)((waves + kWsWaves - 1) / kWsWaves), (unsigned)a.channels);
+    const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
+                        (a.channels == 1 || (nd * 4) % 16 == 0);
+    const size_t lds = (size_t)kWsWaves * 128 * (CB + 16) + sizeof(float) * (7 * 4 * S * S + B * 2 * S);
+    hipLaunchKernelGGL((sos_wscan2_kernel<S, CB>), grid, dim3(kWsThreads), lds, st, (const float*)a.x, (float*)a.y,
+                       (const float*)a.coefs, (const float*)a.P, (const float*)a.Cr, (const float*)a.st_in,
+                       (float*)a.st_out, nd, a.wc, tpw, vec_ok);
+    return hipGetLastError();
+}
+
+template <int CB>
+hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
+    switch (a.sections) {
+        case 1: return launch_wscan2_t<1, CB>(a, st);
+        case 2: return launch_wscan2_t<2, CB>(a, st);
+        case 3: return launch_wscan2_t<3, CB>(a, st);
+        case 4: return launch_wscan2_t<4, CB>(a, st);
+        case 5: return launch_wscan2_t<5, CB>(a, st);
+        case 6: return launch_wscan2_t<6, CB>(a, st);
+        case 7: return launch_wscan2_t<7, CB>(a, st);
+        case 8: return launch_wscan2_t<8, CB>(a, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename C, typename I, int S, int CB>
+hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
+    constexpr int B = ws_chunk<I, CB>::B;
+    const long long nd = (long long)a.n;
+    const long long nch = (nd + B - 1) / B;
+    // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
+    int tpw = (int)(nch / (64LL * 4096));
+    tpw = tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
+    const long long segc = (long long)tpw * 64 - a.wc;
+    const long long waves = (nch + segc - 1) / segc;
+    dim3 grid((unsigned)((waves + kWsWaves - 1) / kWsWaves), (unsigned)a.channels);
+    // 16-byte vector path: aligned bases and channel strides
+    const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
+                        (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
+    const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * 4 * S * S + B * 2 * S);
+    hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
+                       (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
+                       tpw, vec_ok);
+    return hipGetLastError();
+}
+
+template <typename C, typename I, int CB>
+hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
+    switch (a.sections) {
+        case 1: return launch_wscan_t<C, I, 1, CB>(a, st);
+        case 2: return launch_wscan_t<C, I, 2, CB>(a, st);
+        case 3: return launch_wscan_t<C, I, 3, CB>(a, st);
+        case 4: return launch_wscan_t<C, I, 4, CB>(a, st);
+        case 5: return launch_wscan_t<C, I, 5, CB>(a, st);
+        case 6: return launch_wscan_t<C, I, 6, CB>(a, st);
+        case 7: return launch_wscan_t<C, I, 7, CB>(a, st);
+        case 8: return launch_wscan_t<C, I, 8, CB>(a, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+template <typename C, typename I>
+hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
+    if constexpr (std::is_same<I, float>::value) {
+        if (a.ws_variant == 2) return launch_wscan2_s<128>(a, st);
+        if (a.ws_variant == 3) return launch_wscan2_s<64>(a, st);
+    }
+    return a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st) : launch_wscan_s<C, I, 256>(a, st);
+}
+
+}  // namespace
+
+int iir_wscan_chunk(int dtype, int variant) {
+    // variants: 0 = 256-byte chunks, 1 = 128-byte, 2/3 = paired 128/64-byte chunks (real f32 only)
+    if (variant >= 2 && dtype != 0) return 0;
+    const int cb = variant == 0 ? 256 : (variant == 3 ? 64 : 128);
+    switch (dtype) {
+        case 0: return cb / (int)sizeof(float);
+        case 1: return cb / (int)sizeof(c32);
+        case 3: return cb / (int)sizeof(double);
+        case 4: return cb / (int)sizeof(c64);
+    }
+    return 0;
+}
+
+hipError_t launch_iir_wscan(int dtype, const IirArgs& a, hipStream_t st) {
+    if (a.n == 0) return hipSuccess;
+    switch (dtype) {
+        case 0: return launch_wscan_dt<float, float>(a, st);
+        case 1: return launch_wscan_dt<float, c32>(a, st);
+        case 3: return launch_wscan_dt<double, double>(a, st);
+        case 4: return launch_wscan_dt<double, c64>(a, st);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace sdsp

@@ -34,6 +34,10 @@ struct Group {
     int first = 0, count = 0;  // sections [first, first+count)
     int wc = 0;                // warm-up chunks for the scan path (0: scan not applicable)
     DevBuf d_P;                // [8][2c][2c]
+    struct WaveScan {          // wave-scan tables per chunk-size variant (256 B, 128 B)
+        int wc = 0;
+        DevBuf d_P, d_Cr;      // [6][2c][2c], [B][2c] output response to the state
+    } ws[4];
 };
 
 struct DeviceGuardI {
@@ -97,6 +101,7 @@ struct sdsp_iir {
     DevBuf d_coefs, d_state[2], d_tmp[2];
     int cur = 0;
     int algo = SDSP_ALGO_AUTO;
+    int wscan = 1;  // 0: block scan; 1-4: wave-scan variant 0-3 (kern_iir_wscan.hip; sdsp_iir_set_tuning)
     hipStream_t stream = nullptr;
     DevBuf stage_in, stage_out;
     size_t state_per_ch() const { return type == 1 ? (size_t)(2 * S) : (size_t)(cap - 1); }
@@ -157,37 +162,75 @@ Mat sos_A(const sdsp_iir* h, int first, int count) {
     return A;
 }
 
+// Scan tables for chunks of B samples: warm-up chunks wc (smallest m with
+// ||A^(mB)||_inf < tol, m <= max_wc; 0 = the scan is not admissible), P_k =
+// A^(B 2^k) for k < nP, and optionally Cr[i][d] (i < B): the cascade output i
+// steps after starting from basis state e_d with zero input.
+int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, int* wc, DevBuf* dP, DevBuf* dCr) {
+    const double tol = is_f32(h->dtype) ? 1e-9 : 1e-17;
+    const int D = 2 * g.count;
+    const Mat A = sos_A(h, g.first, g.count);
+    const Mat AB = matpow(A, B, D);
+    Mat Am = AB;
+    *wc = 0;
+    for (int m = 1; m <= max_wc; ++m) {
+        const double nrm = norm_inf(Am, D);
+        if (!std::isfinite(nrm)) break;
+        if (nrm < tol) { *wc = m; break; }
+        Am = matmul(Am, AB, D);
+    }
+    if (*wc == 0) return SDSP_OK;
+    std::vector<unsigned char> P;
+    Mat Pk = AB;
+    for (int k = 0; k < nP; ++k) {
+        for (double v : Pk) push_coef(P, v, h->dtype);
+        Pk = matmul(Pk, Pk, D);
+    }
+    IIR_TRY(dP->ensure(P.size()), "alloc P");
+    IIR_TRY(hipMemcpy(dP->p, P.data(), P.size(), hipMemcpyHostToDevice), "copy P");
+    if (!dCr) return SDSP_OK;
+    std::vector<double> resp((size_t)B * D);
+    for (int d = 0; d < D; ++d) {
+        std::vector<double> w1(g.count), w2(g.count);
+        for (int q = 0; q < g.count; ++q) { w1[q] = (2 * q == d) ? 1.0 : 0.0; w2[q] = (2 * q + 1 == d) ? 1.0 : 0.0; }
+        for (int i = 0; i < B; ++i) {
+            double v = 0.0;
+            for (int q = 0; q < g.count; ++q) {
+                const double* c = &h->c64[5 * (g.first + q)];
+                const double w = v - (c[3] * w1[q] + c[4] * w2[q]);
+                v = c[0] * w + c[1] * w1[q] + c[2] * w2[q];
+                w2[q] = w1[q];
+                w1[q] = w;
+            }
+            resp[(size_t)i * D + d] = v;
+        }
+    }
+    std::vector<unsigned char> Cr;
+    for (double v : resp) push_coef(Cr, v, h->dtype);
+    IIR_TRY(dCr->ensure(Cr.size()), "alloc Cr");
+    IIR_TRY(hipMemcpy(dCr->p, Cr.data(), Cr.size(), hipMemcpyHostToDevice), "copy Cr");
+    return SDSP_OK;
+}
+
 int plan_groups(sdsp_iir* h) {
     h->groups.clear();
     if (h->type != 1) return SDSP_OK;
-    const int B = iir_scan_chunk(h->dtype);
-    const double tol = is_f32(h->dtype) ? 1e-9 : 1e-17;
     for (int f = 0; f < h->S; f += kMaxGroupSections) {
         h->groups.emplace_back();
         Group& g = h->groups.back();
         g.first = f;
         g.count = std::min(kMaxGroupSections, h->S - f);
-        const int D = 2 * g.count;
-        const Mat A = sos_A(h, g.first, g.count);
-        const Mat AB = matpow(A, B, D);
-        // warm-up: smallest m with ||A^(mB)||_inf < tol, m <= lanes/2
-        Mat Am = AB;
-        g.wc = 0;
-        for (int m = 1; m <= kScanLanes / 2; ++m) {
-            const double nrm = norm_inf(Am, D);
-            if (!std::isfinite(nrm)) break;
-            if (nrm < tol) { g.wc = m; break; }
-            Am = matmul(Am, AB, D);
-        }
+        // block scan (kern_iir.hip): 8 powers, warm-up up to half the block's lanes
+        int st = scan_tables(h, g, iir_scan_chunk(h->dtype), kScanLanes / 2, 8, &g.wc, &g.d_P, nullptr);
+        if (st) return st;
         if (g.wc == 0) continue;
-        std::vector<unsigned char> P;
-        Mat Pk = AB;
-        for (int k = 0; k < 8; ++k) {
-            for (double v : Pk) push_coef(P, v, h->dtype);
-            Pk = matmul(Pk, Pk, D);
+        // wave scan (kern_iir_wscan.hip), one table set per chunk size: 6 powers, warm-up <= 32 chunks
+        for (int v = 0; v < 4; ++v) {
+            const int Bw = iir_wscan_chunk(h->dtype, v);
+            if (Bw == 0) continue;
+            st = scan_tables(h, g, Bw, 32, 7, &g.ws[v].wc, &g.ws[v].d_P, &g.ws[v].d_Cr);
+            if (st) return st;
         }
-        IIR_TRY(g.d_P.ensure(P.size()), "alloc P");
-        IIR_TRY(hipMemcpy(g.d_P.p, P.data(), P.size(), hipMemcpyHostToDevice), "copy P");
     }
     return SDSP_OK;
 }
@@ -335,7 +378,10 @@ void sdsp_iir_destroy(sdsp_iir* h) {
         }
         h->d_coefs.release();
         for (int i = 0; i < 2; ++i) { h->d_state[i].release(); h->d_tmp[i].release(); }
-        for (auto& g : h->groups) g.d_P.release();
+        for (auto& g : h->groups) {
+            g.d_P.release();
+            for (auto& w : g.ws) { w.d_P.release(); w.d_Cr.release(); }
+        }
         h->stage_in.release();
         h->stage_out.release();
     }
@@ -351,6 +397,7 @@ int sdsp_iir_clone(const sdsp_iir* h, sdsp_iir** out) {
     sdsp_iir* c = *out;
     DeviceGuardI g(h->device);
     c->algo = h->algo;
+    c->wscan = h->wscan;
     if (h->channels != 1) {
         st = sdsp_iir_set_channels(c, h->channels);
         if (st) return st;
@@ -373,6 +420,14 @@ int sdsp_iir_set_channels(sdsp_iir* h, size_t channels) {
 int sdsp_iir_set_algo(sdsp_iir* h, int algo) {
     if (!h || !(algo == SDSP_ALGO_AUTO || algo == SDSP_ALGO_EXACT || algo == SDSP_ALGO_FMA)) return SDSP_E_INVALID_ARGUMENT;
     h->algo = algo;  // FMA = always the block-parallel scan where the cascade admits it
+    return SDSP_OK;
+}
+
+int sdsp_iir_set_tuning(sdsp_iir* h, int key, int value) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (key != SDSP_TUNE_IIR_WAVE_SCAN) return SDSP_E_INVALID_ARGUMENT;
+    if (value < 0 || value > 4) return SDSP_E_INVALID_ARGUMENT;
+    h->wscan = value;
     return SDSP_OK;
 }
 
@@ -427,7 +482,16 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
             IirArgs a{src, dst, (const unsigned char*)h->d_coefs.p + 5 * gr.first * cb, gr.d_P.p,
                       st_in + soff, st_out + soff, n_g, last ? nout : nd, h->channels, gr.count, 0, 0, 0,
                       first ? Mi : 1, last ? Md : 1, last ? h->phase : 0, group_scan(h, gr, nd), gr.wc};
-            IIR_TRY(launch_iir(h->dtype, a, s), "iir sos");
+            const int wv = h->wscan - 1;
+            if (a.algo_scan && a.Mi == 1 && a.Md == 1 && wv >= 0 && gr.ws[wv].wc > 0) {
+                a.P = gr.ws[wv].d_P.p;
+                a.Cr = gr.ws[wv].d_Cr.p;
+                a.wc = gr.ws[wv].wc;
+                a.ws_variant = wv;
+                IIR_TRY(launch_iir_wscan(h->dtype, a, s), "iir sos wave scan");
+            } else {
+                IIR_TRY(launch_iir(h->dtype, a, s), "iir sos");
+            }
             soff += h->channels * 2 * gr.count * sbytes;
             src = dst;
         }

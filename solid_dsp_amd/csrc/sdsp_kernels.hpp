@@ -69,9 +69,14 @@ struct IirArgs {
     size_t phase;        // DecimatingIIRFilter index before this block
     bool algo_scan;
     int wc;              // warm-up chunks (scan)
+    const void* Cr = nullptr;  // wave scan: [B][2S] output response to the state, c A^i (Coef type)
+    int ws_variant = 0;        // wave scan chunk: 0 = 256 bytes, 1 = 128 bytes
 };
 hipError_t launch_iir(int dtype, const IirArgs& a, hipStream_t s);
 int iir_scan_chunk(int dtype);  // samples per lane chunk of the scan kernel
+// wave-level scan (kern_iir_wscan.hip): SOS, no decimation/interpolation, wc <= 32
+hipError_t launch_iir_wscan(int dtype, const IirArgs& a, hipStream_t s);
+int iir_wscan_chunk(int dtype, int variant);  // samples per lane chunk of the wave scan
 
 // batched FFT (power of two: Stockham in LDS; otherwise direct DFT)
 struct FftArgs {

@@ -193,6 +193,51 @@ def test_scan_cfg3_cascade_tolerance(dt, cdt, sdt):
     assert np.abs(y - ref).max() <= tol * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("dt,cdt,sdt", DT)
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+def test_scan_kernel_variants(dt, cdt, sdt, variant):
+    # block scan (0) and the wave-scan variants (1: 256-byte chunks, 2: 128-byte, 3/4: paired
+    # 128/64-byte chunks, real f32 only; elsewhere the handle falls back to the block scan):
+    # many segments, ragged streaming calls, against the f64 restatement
+    ff, fb = butter()
+    f = IIRFilter(ff.astype(cdt), fb.astype(cdt), SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    assert sd.lib().sdsp_iir_set_tuning(f._h, 7, variant) == 0
+    n = 1500001
+    x = O.synth(20250226, 7, 0, n, complex_=np.dtype(sdt).kind == "c").astype(sdt)
+    parts = [0, 1, 4097, 1000003, n]
+    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(parts[:-1], parts[1:])])
+    wide = np.complex128 if np.dtype(sdt).kind == "c" else np.float64
+    ref = O.iir(O.RC64 if np.dtype(sdt).kind == "c" else O.RR64, ff.astype(cdt).astype(np.float64),
+                fb.astype(cdt).astype(np.float64), O.SECOND_ORDER).execute_block(x.astype(wide))
+    tol = 1e-5 if cdt == np.float32 else 1e-12
+    assert rel_rms(y, ref) <= tol
+    assert np.abs(y - ref).max() <= tol * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+def test_scan_multi_tile_segments(variant):
+    # 2^26 real f32 samples: several tiles per wave (cross-tile carry, prefetch), checked
+    # against the block scan on the whole stream and the f64 restatement on its head and tail
+    import torch
+    ff, fb = butter()
+    ff, fb = ff.astype(np.float32), fb.astype(np.float32)
+    n = 1 << 26
+    d_in = torch.empty(n, dtype=torch.float32, device="cuda")
+    sd.lib().sdsp_synth_f32_device(d_in.data_ptr(), 99, 0, 0, n, None)
+    outs = []
+    for v in (0, variant):
+        f = IIRFilter(ff, fb, SO, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+        assert sd.lib().sdsp_iir_set_tuning(f._h, 7, v) == 0
+        d_out = torch.empty_like(d_in)
+        f.execute_block_device(d_in, n, d_out, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        outs.append(d_out.cpu().numpy().astype(np.float64))
+    assert rel_rms(outs[1], outs[0]) <= 1e-5
+    x = d_in[: 1 << 20].cpu().numpy().astype(np.float64)
+    ref = O.iir(O.RR64, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER).execute_block(x)
+    assert rel_rms(outs[1][: 1 << 20], ref) <= 1e-5
+
+
 def test_scan_decim_interp_and_state_carry():
     ff, fb = butter()
     x = O.synth(11, 0, 0, 100000)

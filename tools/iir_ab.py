@@ -1,0 +1,54 @@
+"""Interleaved in-process A/B of the SOS scan kernels (block scan vs wave scan,
+SDSP_TUNE_IIR_WAVE_SCAN) on the cfg3 workload, with agreement between them."""
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main(rounds=8, log2n=30):
+    import torch
+    import solid_dsp_amd as sd
+    from solid_dsp_amd import IIRFilter, IIRFilterType
+    n = 1 << log2n
+    sos = np.array(json.load(open(os.path.join(REPO, "tests", "golden", "butter8_0p2_sos.json")))["sos"])
+    ff = sos[:, :3].reshape(-1).astype(np.float32)
+    fb = sos[:, 3:].reshape(-1).astype(np.float32)
+    d_in = torch.empty(n, dtype=torch.float32, device="cuda")
+    sd.lib().sdsp_synth_f32_device(d_in.data_ptr(), 20250226, 0, 0, n, None)
+    s = torch.cuda.current_stream()
+    variants, outs = {}, {}
+    for ws in (0, 1, 2, 3, 4):
+        f = IIRFilter(ff, fb, IIRFilterType.SecondOrder, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+        sd.lib().sdsp_iir_set_tuning(f._h, 7, ws)
+        variants[f"wscan{ws}"] = f
+        o = torch.empty_like(d_in)
+        f.execute_block_device(d_in, n, o, s)
+        torch.cuda.synchronize()
+        outs[f"wscan{ws}"] = (o[: 1 << 22].cpu().numpy().astype(np.float64), o[-(1 << 20):].cpu().numpy().astype(np.float64))
+        f.reset()
+    a = outs["wscan0"]
+    agree = {k: max(float(np.linalg.norm(a[i] - b[i]) / np.linalg.norm(a[i])) for i in range(2))
+             for k, b in outs.items()}
+    d_out = torch.empty_like(d_in)
+    times = {k: [] for k in variants}
+    for _ in range(rounds):
+        for k, f in variants.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            f.execute_block_device(d_in, n, d_out, s)
+            e1.record(s)
+            torch.cuda.synchronize()
+            times[k].append(e0.elapsed_time(e1))
+    res = {k: {"median_ms": float(np.median(v)), "GBps": 8.0 * n / (np.median(v) * 1e-3) / 1e9}
+           for k, v in times.items()}
+    res["rel_rms_between"] = agree
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
