@@ -148,6 +148,7 @@ def _optional_sigs():
         "sdsp_iir_set_channels": (i, [vp, sz]),
         "sdsp_iir_set_algo": (i, [vp, i]),
         "sdsp_iir_set_tuning": (i, [vp, i, i]),
+        "sdsp_chan_set_tuning": (i, [vp, i, i]),
         "sdsp_iir_output_count": (sz, [vp, sz]),
         "sdsp_iir_execute_block": (i, [vp, vp, sz, vp, szp]),
         "sdsp_iir_execute_block_device": (i, [vp, vp, sz, vp, szp, vp]),

@@ -93,6 +93,7 @@ struct sdsp_chan {
     std::vector<unsigned char> taps;
     DevBuf cb, tw, hist[2], stage_in, stage_out;
     int cur = 0;
+    bool fast = true;  // streaming M = 1024 kernel (SDSP_TUNE_CHAN_STREAMING)
     hipStream_t stream = nullptr;
 };
 
@@ -237,6 +238,12 @@ int sdsp_chan_set_streams(sdsp_chan* h, size_t streams) {
     return SDSP_OK;
 }
 
+int sdsp_chan_set_tuning(sdsp_chan* h, int key, int value) {
+    if (!h || key != SDSP_TUNE_CHAN_STREAMING) return SDSP_E_INVALID_ARGUMENT;
+    h->fast = value != 0;
+    return SDSP_OK;
+}
+
 int sdsp_chan_reset(sdsp_chan* h) { return h ? sdsp_chan_set_streams(h, h->streams) : SDSP_E_INVALID_ARGUMENT; }
 
 int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, void* d_out, size_t* frames,
@@ -252,6 +259,7 @@ int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, voi
     Guard g(h->device);
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     ChanArgs a{d_in, h->hist[h->cur].p, h->cb.p, d_out, h->tw.p, (int)h->M, ilog2(h->M), (int)h->K, n, fr, h->streams};
+    a.fast = h->fast;
     F_TRY(launch_chan(h->dtype == SDSP_RC64, a, s), "channeliser");
     const int H = (int)((h->K - 1) * h->M);
     F_TRY(launch_hist_update(h->dtype, d_in, h->hist[h->cur].p, h->hist[h->cur ^ 1].p, n, H, h->streams, s),

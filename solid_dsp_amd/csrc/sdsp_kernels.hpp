@@ -98,8 +98,11 @@ struct ChanArgs {
     const void* tw;
     int M, logM, K;
     size_t n, frames, streams;
+    bool fast = true;  // use the streaming kernel where it applies (sdsp_chan_set_tuning)
 };
 hipError_t launch_chan(bool f64, const ChanArgs& a, hipStream_t s);
+// streaming M = 1024 kernel (kern_chan1024.hip); false = not applicable
+bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err);
 
 // batched DotProduct::execute
 struct DotArgs {
