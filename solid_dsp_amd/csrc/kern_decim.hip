@@ -207,10 +207,10 @@ template <typename C, typename I, int M, int K, int V>
 hipError_t launch_poly_t(const FirArgs& a, hipStream_t s) {
     using Geo = PolyGeom<I, M, K, V>;
     const long long nout = (long long)a.nout;
-    // outputs per group: a multiple of CH; ~64-256 measured best on cfg4 (short
-    // segments keep the concurrently streamed address range compact)
+    // outputs per group: a multiple of CH.  64-256 measured fastest on cfg4; 256 keeps the
+    // K warm-up rows per group (re-read input) to ~3% of the traffic
     long long seg = a.seg > 0 ? a.seg : (nout + 8191) / 8192;
-    if (a.seg <= 0 && seg > 64) seg = 64;
+    if (a.seg <= 0 && seg > 256) seg = 256;
     seg = (seg + Geo::CH - 1) / Geo::CH * Geo::CH;
     if (seg < Geo::CH) seg = Geo::CH;
     const long long groups = (nout + seg - 1) / seg;

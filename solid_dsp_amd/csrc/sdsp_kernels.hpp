@@ -99,6 +99,7 @@ struct ChanArgs {
     int M, logM, K;
     size_t n, frames, streams;
     bool fast = true;  // use the streaming kernel where it applies (sdsp_chan_set_tuning)
+    int frames_per_block = 0;  // streaming kernel: frames per workgroup (0 = default)
 };
 hipError_t launch_chan(bool f64, const ChanArgs& a, hipStream_t s);
 // streaming M = 1024 kernel (kern_chan1024.hip); false = not applicable

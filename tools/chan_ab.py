@@ -21,17 +21,19 @@ def main(rounds=6):
         sd.lib().sdsp_synth_f32_device(d_in[s_ * n:].data_ptr(), 20250226, s_, 0, 2 * n, None)
     st = torch.cuda.current_stream()
     variants, outs = {}, {}
-    for fast in (0, 1):
+    for fast, fpb in ((0, 0), (1, 32), (1, 64), (1, 128), (1, 256)):
         f = Channelizer(h, M, sample_dtype=np.complex64, streams=S)
         assert sd.lib().sdsp_chan_set_tuning(f._h, 8, fast) == 0
-        variants[f"fast{fast}"] = f
+        assert sd.lib().sdsp_chan_set_tuning(f._h, 9, fpb) == 0
+        key = f"fast{fast}_fpb{fpb}"
+        variants[key] = f
         o = torch.empty_like(d_in)
         f.execute_block_device(d_in, n, o, st)
         torch.cuda.synchronize()
-        outs[f"fast{fast}"] = o.cpu().numpy().astype(np.complex128)
+        outs[key] = o.cpu().numpy().astype(np.complex128)
         f.reset()
-    a, b = outs["fast0"], outs["fast1"]
-    agree = float(np.linalg.norm(a - b) / np.linalg.norm(a))
+    a = outs["fast0_fpb0"]
+    agree = {k: float(np.linalg.norm(a - b) / np.linalg.norm(a)) for k, b in outs.items()}
     d_out = torch.empty_like(d_in)
     times = {k: [] for k in variants}
     for _ in range(rounds):
