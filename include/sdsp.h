@@ -115,18 +115,20 @@ SDSP_API int sdsp_fir_set_algo(sdsp_fir* h, int algo);
 SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
 /* kernel-variant knobs (performance only; results are identical across values, except
  * SDSP_TUNE_OLS_ABLATE_NOMEM, a profiling ablation that skips HBM traffic and leaves the
- * output unwritten) */
+ * output unwritten).  WIDE / DEPTH2 / OCCUPANCY name overlap-save variants that were
+ * measured slower and retired: only 0 is accepted (SDSP_E_UNSUPPORTED otherwise). */
 typedef enum {
     SDSP_TUNE_OLS_WIDE = 1,
-    SDSP_TUNE_OLS_INTERLEAVE = 2,
+    SDSP_TUNE_OLS_INTERLEAVE = 2,  /* 1 (default): segments interleaved across the persistent grid */
     SDSP_TUNE_OLS_DEPTH2 = 3,
     SDSP_TUNE_OLS_ABLATE_NOMEM = 4,
-    SDSP_TUNE_OLS_OCCUPANCY = 5, /* 0 = 2-wave kernel, 3/4 = single-region kernel at 3/4 blocks per CU */
+    SDSP_TUNE_OLS_OCCUPANCY = 5,
     SDSP_TUNE_DECIM_SEG = 6,     /* FMA decimator: outputs per lane group (0 = automatic) */
     SDSP_TUNE_IIR_WAVE_SCAN = 7, /* IIR scan kernel: 0 = block scan, 1 (default) = wave scan with 256-byte chunks,
                                     2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */
     SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: 1 (default) = streaming M=1024 kernel where it applies, 0 = per-frame */
-    SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9 /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
+    SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
+    SDSP_TUNE_OLS_NONTEMPORAL = 10  /* overlap-save streaming loads (bit 0) / stores (bit 1) */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */

@@ -32,6 +32,7 @@ namespace sdsp {
 namespace {
 
 struct cf { float re, im; };
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ cf cadd(cf a, cf b) { return {a.re + b.re, a.im + b.im}; }
 __device__ __forceinline__ cf csub(cf a, cf b) { return {a.re - b.re, a.im - b.im}; }
@@ -105,17 +106,6 @@ constexpr int kRegion = 16 * kRowA;  // samples per LDS region
 // B image: 256 rows x 16 samples, pairs XOR-swizzled by (row>>1)&7
 __device__ __forceinline__ int bidx(int r, int c) { return r * 16 + ((((c >> 1) ^ (r >> 1)) & 7) << 1) + (c & 1); }
 
-// ---- 16-byte-per-lane global access --------------------------------------
-// Lane t needs x[base + 256 r + t] for rows r = 0..15 (8 bytes, coalesced).
-// For a row pair (a, b) = (2q, 2q+1) an even lane reads x[base+256a+t .. +1]
-// and an odd lane x[base+256b+t-1 .. +1], each one 16-byte access; one DPP
-// swap between lanes t and t^1 then gives every lane its own two values.
-// Stores use the inverse.  base and V are even, so every 16-byte access is
-// aligned.
-__device__ __forceinline__ float swap_pair(float v) {  // value of lane t^1 (DPP quad_perm [1,0,3,2])
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
-}
-
 template <bool CHECK>
 __device__ __forceinline__ cf ext_ld(const cf* __restrict__ x, const cf* __restrict__ hist, long long j, long long n,
                                      int Lm1) {
@@ -132,68 +122,83 @@ __device__ __forceinline__ cf ext_ld(const cf* __restrict__ x, const cf* __restr
     }
 }
 
-// raw[q] = the 16 bytes this lane reads for row pair q
-template <bool CHECK>
-__device__ __forceinline__ void load_raw(float4 (&raw)[8], const cf* __restrict__ x, const cf* __restrict__ hist,
-                                         long long base, int t, long long n, int Lm1) {
-    const int odd = t & 1;
+// P1..P5 of one segment on v (loaded: lane t holds x over n2).  `after_p1` runs
+// right after P1's LDS writes (the next segment's loads go out there).  On return
+// v holds the segment's outputs over rows n2.
+template <typename F>
+__device__ __forceinline__ void ols_segment(cf (&v)[16], cf* __restrict__ rA, cf* __restrict__ rB,
+                                            const cf (&w1)[16], const cf (&w2)[16], const cf (&Hr)[16], int t,
+                                            F&& after_p1) {
+    const int hi4 = t >> 4, lo4 = t & 15;
+    // P1: DFT over n2 -> k0, twiddle, A[k0][t]
+    dft16<false>(v);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const long long j = base + 256 * (2 * q + odd) + t - odd;  // even index
-        if constexpr (!CHECK) {
-            raw[q] = *reinterpret_cast<const float4*>(x + j);
-        } else {
-            const cf a = ext_ld<true>(x, hist, j, n, Lm1), b = ext_ld<true>(x, hist, j + 1, n, Lm1);
-            raw[q] = make_float4(a.re, a.im, b.re, b.im);
+    for (int k = 0; k < 16; ++k) rA[k * kRowA + t] = cmul(v[k], w1[k]);
+    after_p1();
+    __syncthreads();
+    // P2: lane (k0=hi4, n0=lo4) reads n1
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = rA[hi4 * kRowA + 16 * k + lo4];
+    dft16<false>(v);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) rB[bidx(16 * hi4 + k, lo4)] = cmul(v[k], w2[k]);
+    __syncthreads();
+    // P3: lane (k0=hi4, k1=lo4) reads its row over n0
+    {
+        const float4* row = reinterpret_cast<const float4*>(rB + t * 16);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const float4 q = row[(p ^ (t >> 1)) & 7];
+            v[2 * p] = {q.x, q.y};
+            v[2 * p + 1] = {q.z, q.w};
         }
     }
-}
-
-__device__ __forceinline__ void unpack_raw(cf (&v)[16], const float4 (&raw)[8], int t) {
-    const bool odd = t & 1;
+    dft16<false>(v);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const float4 r = raw[q];
-        // even lane sends its partner's row-a value (hi), odd lane its partner's row-b value (lo)
-        const float sre = odd ? r.x : r.z, sim = odd ? r.y : r.w;
-        const float gre = swap_pair(sre), gim = swap_pair(sim);
-        v[2 * q] = odd ? cf{gre, gim} : cf{r.x, r.y};
-        v[2 * q + 1] = odd ? cf{r.z, r.w} : cf{gre, gim};
-    }
-}
-
-// store rows >= h2 of v (row r at y[ob + 256 r], ob = segment output base + t)
-template <bool CHECK>
-__device__ __forceinline__ void store_rows(cf* __restrict__ y, const cf (&v)[16], long long ob, int t, int h2,
-                                           long long n) {
-    const bool odd = t & 1;
+    for (int k = 0; k < 16; ++k) v[k] = cmul(v[k], Hr[k]);
+    dft16<true>(v);
+    // back to A region (its readers all passed the barrier above)
+    {
+        float4* row = reinterpret_cast<float4*>(rA + t * 16);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const cf a = v[2 * q], b = v[2 * q + 1];
-        // even lane needs the odd partner's row-a value, odd lane the even partner's row-b value
-        const float sre = odd ? a.re : b.re, sim = odd ? a.im : b.im;
-        const float gre = swap_pair(sre), gim = swap_pair(sim);
-        const int row = 2 * q + (odd ? 1 : 0);
-        const long long j = ob + 256 * row - (odd ? 1 : 0);  // even index
-        const float4 w = odd ? make_float4(gre, gim, b.re, b.im) : make_float4(a.re, a.im, gre, gim);
-        if (row >= h2) {
-            if constexpr (!CHECK) {
-                *reinterpret_cast<float4*>(y + j) = w;
-            } else {
-                if (j >= 0 && j < n) y[j] = cf{w.x, w.y};
-                if (j + 1 >= 0 && j + 1 < n) y[j + 1] = cf{w.z, w.w};
-            }
+        for (int p = 0; p < 8; ++p) {
+            const cf a = cmulc(v[2 * p], w2[2 * p]);
+            const cf b = cmulc(v[2 * p + 1], w2[2 * p + 1]);
+            row[(p ^ (t >> 1)) & 7] = make_float4(a.re, a.im, b.re, b.im);
         }
     }
+    __syncthreads();
+    // P4: lane (k0=hi4, n0=lo4) reads k1
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = rA[bidx(16 * hi4 + k, lo4)];
+    dft16<true>(v);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) rB[hi4 * kRowA + 16 * k + lo4] = v[k];
+    __syncthreads();
+    // P5: lane t=(n1,n0) reads k0
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = cmulc(rB[k * kRowA + t], w1[k]);
+    dft16<true>(v);
+    // the next segment's P1 writes region A: every lane has finished reading
+    // region A (P4) before the barrier that precedes P5.
 }
 
 }  // namespace
 
-template <bool WIDE, bool INTERLEAVE, bool DEPTH2, bool NOMEM = false>
+// Segments are split into interior ones (input window [base, base+4096) and
+// all outputs inside the stream) and at most a first and a last boundary
+// segment.  The main loop runs interior segments only, with straight-line
+// loads and stores and an unconditional one-segment-ahead prefetch, so the
+// compiler's wait for the prefetched data at the loop head counts only the
+// loads (vmcnt(16 stores)) instead of draining every store (vmcnt(0)).
+// H2 > 0: halo rows known at compile time (the interior stores are then
+// unconditional and the loop-head wait counts them exactly); H2 = 0: runtime h2.
+template <bool INTERLEAVE, int ABL, int H2, int NT = 0>
 __global__ void __launch_bounds__(256, 2)
 fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const cf* __restrict__ Hs,
                    const cf* __restrict__ tw1, const cf* __restrict__ tw2, cf* __restrict__ y, long long n,
-                   int Lm1, int h2, long long nseg, long long segs_per_block) {
+                   int Lm1, int h2_rt, long long nseg, long long segs_per_block) {
+    const int h2 = H2 > 0 ? H2 : h2_rt;
     __shared__ __attribute__((aligned(16))) cf lds[2 * kRegion];
     cf* const rA = lds;
     cf* const rB = lds + kRegion;
@@ -203,7 +208,7 @@ fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const 
     hist += (long long)ch * Lm1;
 
     const int t = threadIdx.x;
-    const int hi4 = t >> 4, lo4 = t & 15;
+    const int lo4 = t & 15;
     cf w1[16], w2[16], Hr[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -228,239 +233,92 @@ fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const 
         if (s1 > nseg) s1 = nseg;
         sstep = 1;
     }
+    auto base_of = [&](long long sg) { return sg * V - 256 * h2; };
+    auto interior = [&](long long sg) { return sg < s1 && base_of(sg) >= 0 && base_of(sg) + 4096 <= n; };
 
-    // software pipeline: the next segment's loads are issued right after this
-    // segment's P1 and land while P2..P5 run (2 waves/SIMD cannot hide HBM
-    // latency otherwise)
-    float4 nx[8];
-    cf nv[16], nv2[16];
-    auto load_plain = [&](cf (&dst)[16], long long sg) {
-        const long long base = sg * V - 256 * h2;
-        if constexpr (NOMEM) {  // ablation build: no HBM traffic, same arithmetic
+    // boundary segment: guarded element loads and stores, no prefetch
+    auto boundary = [&](long long sg) {
+        cf v[16];
+        const long long base = base_of(sg);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) dst[r] = cf{(float)(t + r), (float)(sg & 1023)};
-            return;
-        }
-        // branch once per segment: a per-element "load or select" makes hipcc
-        // wait for every load separately
-        if (base >= 0 && base + 4096 <= n) {
+        for (int r = 0; r < 16; ++r) v[r] = ext_ld<true>(x, hist, base + 256 * r + t, n, Lm1);
+        ols_segment(v, rA, rB, w1, w2, Hr, t, [] {});
+        const long long ob = base + t;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) dst[r] = x[base + 256 * r + t];
+        for (int k = 0; k < 16; ++k)
+            if (k >= h2 && ob + 256 * k < n) y[ob + 256 * k] = v[k];
+        __syncthreads();  // region A/B reuse by the next segment
+    };
+
+    long long seg = s0;
+    if (seg < s1 && !interior(seg)) {
+        boundary(seg);
+        seg += sstep;
+    }
+    cf nv[16];
+    auto load = [&](long long sg) {
+        if constexpr (ABL == 1 || ABL == 2) {  // ablation builds: no input traffic, same arithmetic
+#pragma unroll
+            for (int r = 0; r < 16; ++r) nv[r] = cf{(float)(t + r), (float)(sg & 1023)};
         } else {
+            const cf* xb = x + base_of(sg);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) dst[r] = ext_ld<true>(x, hist, base + 256 * r + t, n, Lm1);
+            for (int r = 0; r < 16; ++r) {
+                if constexpr (NT & 1) {  // streaming loads
+                    const f2v q = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(xb + 256 * r + t));
+                    nv[r] = cf{q.x, q.y};
+                } else {
+                    nv[r] = xb[256 * r + t];
+                }
+            }
         }
     };
-    auto prefetch = [&](long long sg) {
-        if constexpr (WIDE) {
-            const long long base = sg * V - 256 * h2;
-            if (base >= 0 && base + 4096 <= n) load_raw<false>(nx, x, hist, base, t, n, Lm1);
-            else load_raw<true>(nx, x, hist, base, t, n, Lm1);
-        } else if constexpr (DEPTH2) {
+    // Interior segments.  Stores are deferred by one segment: segment s's outputs
+    // go out after P1 of segment s+1, ahead of the loads for segment s+2, so the
+    // loop-head wait for those loads never waits on freshly issued stores.
+    cf ov[16];
+    long long oseg = -1;
+    auto store_out = [&]() {
+        cf* yb = y + base_of(oseg) + t;
+        if constexpr (ABL == 1 || ABL == 3) {  // ablation builds: no output traffic
 #pragma unroll
-            for (int r = 0; r < 16; ++r) nv[r] = nv2[r];
-            if (sg + sstep < s1) load_plain(nv2, sg + sstep);
+            for (int k = 0; k < 16; ++k)
+                if (ov[k].re == 1234.5678f && k >= h2) yb[256 * k] = ov[k];
         } else {
-            load_plain(nv, sg);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (k >= h2) {
+                    if constexpr (NT & 2) __builtin_nontemporal_store(f2v{ov[k].re, ov[k].im}, reinterpret_cast<f2v*>(yb + 256 * k));
+                    else yb[256 * k] = ov[k];
+                }
+            }
         }
     };
-    if (s0 < s1) {
-        if constexpr (!WIDE && DEPTH2) {
-            load_plain(nv2, s0);
-            prefetch(s0);
-        } else {
-            prefetch(s0);
-        }
-    }
-    for (long long seg = s0; seg < s1; seg += sstep) {
+    if (interior(seg)) load(seg);
+    for (; interior(seg); seg += sstep) {
         cf v[16];
-        if constexpr (WIDE) {
-            unpack_raw(v, nx, t);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = nv[r];
+        // next interior segment, or this one again (keeps the loop body uniform)
+        const long long nxt = interior(seg + sstep) ? seg + sstep : seg;
+        if constexpr (NT & 4) {
+            ols_segment(v, rA, rB, w1, w2, Hr, t, [&] { load(nxt); });
+#pragma unroll
+            for (int k = 0; k < 16; ++k) ov[k] = v[k];
+            oseg = seg;
+            store_out();
         } else {
+            ols_segment(v, rA, rB, w1, w2, Hr, t, [&] {
+                if (oseg >= 0) store_out();
+                load(nxt);
+            });
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = nv[r];
-        }
-
-        // P1: DFT over n2 -> k0, twiddle, A[k0][t]
-        dft16<false>(v);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) rA[k * kRowA + t] = cmul(v[k], w1[k]);
-        if (seg + sstep < s1) prefetch(seg + sstep);
-        __syncthreads();
-        // P2: lane (k0=hi4, n0=lo4) reads n1
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = rA[hi4 * kRowA + 16 * k + lo4];
-        dft16<false>(v);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) rB[bidx(16 * hi4 + k, lo4)] = cmul(v[k], w2[k]);
-        __syncthreads();
-        // P3: lane (k0=hi4, k1=lo4) reads its row over n0
-        {
-            const float4* row = reinterpret_cast<const float4*>(rB + t * 16);
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const float4 q = row[(p ^ (t >> 1)) & 7];
-                v[2 * p] = {q.x, q.y};
-                v[2 * p + 1] = {q.z, q.w};
-            }
-        }
-        dft16<false>(v);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = cmul(v[k], Hr[k]);
-        dft16<true>(v);
-        // back to A region (its readers all passed the barrier above)
-        {
-            float4* row = reinterpret_cast<float4*>(rA + t * 16);
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const cf a = cmulc(v[2 * p], w2[2 * p]);
-                const cf b = cmulc(v[2 * p + 1], w2[2 * p + 1]);
-                row[(p ^ (t >> 1)) & 7] = make_float4(a.re, a.im, b.re, b.im);
-            }
-        }
-        __syncthreads();
-        // P4: lane (k0=hi4, n0=lo4) reads k1
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = rA[bidx(16 * hi4 + k, lo4)];
-        dft16<true>(v);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) rB[hi4 * kRowA + 16 * k + lo4] = v[k];
-        __syncthreads();
-        // P5: lane t=(n1,n0) reads k0
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = cmulc(rB[k * kRowA + t], w1[k]);
-        dft16<true>(v);
-        const long long ob = seg * V - 256 * h2 + t;
-        if constexpr (NOMEM) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (v[k].re == 1234.5678f && k >= h2) y[ob + 256 * k] = v[k];
-        } else if constexpr (WIDE) {
-            if (ob - 1 >= 0 && ob + 256 * 16 <= n) store_rows<false>(y, v, ob, t, h2, n);
-            else store_rows<true>(y, v, ob, t, h2, n);
-        } else {
-            if (ob + 256 * 16 <= n) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    if (k >= h2) y[ob + 256 * k] = v[k];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    if (k >= h2 && ob + 256 * k < n) y[ob + 256 * k] = v[k];
-            }
-        }
-        // next segment's P1 writes region A: every lane has finished reading
-        // region A (P4) before the barrier that precedes P5.
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Occupancy variant: one LDS region (8 barriers per segment), the spectrum
-// slice read from L2 inside P3 instead of living in registers, no register
-// prefetch (thread-level parallelism hides the loads instead).  Targets 3-4
-// waves per SIMD: the 2-wave kernel above is VALU-issue bound (an ablation
-// without HBM traffic runs at 80% of its time).
-template <int WAVES_PER_SIMD, bool NOMEM>
-__global__ void __launch_bounds__(256, WAVES_PER_SIMD)
-fir_ols4096_occ_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const cf* __restrict__ Hs,
-                       const cf* __restrict__ tw1, const cf* __restrict__ tw2, cf* __restrict__ y, long long n,
-                       int Lm1, int h2, long long nseg) {
-    __shared__ __attribute__((aligned(16))) cf lds[kRegion];
-    const int ch = blockIdx.y;
-    x += (long long)ch * n;
-    y += (long long)ch * n;
-    hist += (long long)ch * Lm1;
-    const int t = threadIdx.x;
-    const int hi4 = t >> 4, lo4 = t & 15;
-    cf w1[16], w2[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        w1[k] = tw1[t * 16 + k];
-        w2[k] = tw2[lo4 * 16 + k];
-    }
-    const int V = 4096 - 256 * h2;
-    for (long long seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-        cf v[16];
-        const long long base = seg * V - 256 * h2;
-        if constexpr (NOMEM) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = cf{(float)(t + r), (float)(seg & 1023)};
-        } else if (base >= 0 && base + 4096 <= n) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = x[base + 256 * r + t];
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = ext_ld<true>(x, hist, base + 256 * r + t, n, Lm1);
-        }
-        // P1
-        dft16<false>(v);
-        __syncthreads();  // previous segment's P5 reads of the region are done
-#pragma unroll
-        for (int k = 0; k < 16; ++k) lds[k * kRowA + t] = cmul(v[k], w1[k]);
-        __syncthreads();
-        // P2
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = lds[hi4 * kRowA + 16 * k + lo4];
-        dft16<false>(v);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) lds[bidx(16 * hi4 + k, lo4)] = cmul(v[k], w2[k]);
-        __syncthreads();
-        // P3
-        {
-            const float4* row = reinterpret_cast<const float4*>(lds + t * 16);
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const float4 q = row[(p ^ (t >> 1)) & 7];
-                v[2 * p] = {q.x, q.y};
-                v[2 * p + 1] = {q.z, q.w};
-            }
-        }
-        cf Hr[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) Hr[k] = Hs[t * 16 + k];
-        dft16<false>(v);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = cmul(v[k], Hr[k]);
-        dft16<true>(v);
-        __syncthreads();
-        {
-            float4* row = reinterpret_cast<float4*>(lds + t * 16);
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-                const cf a = cmulc(v[2 * p], w2[2 * p]);
-                const cf b = cmulc(v[2 * p + 1], w2[2 * p + 1]);
-                row[(p ^ (t >> 1)) & 7] = make_float4(a.re, a.im, b.re, b.im);
-            }
-        }
-        __syncthreads();
-        // P4
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = lds[bidx(16 * hi4 + k, lo4)];
-        dft16<true>(v);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 16; ++k) lds[hi4 * kRowA + 16 * k + lo4] = v[k];
-        __syncthreads();
-        // P5
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = cmulc(lds[k * kRowA + t], w1[k]);
-        dft16<true>(v);
-        const long long ob = seg * V - 256 * h2 + t;
-        if constexpr (NOMEM) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (v[k].re == 1234.5678f && k >= h2) y[ob + 256 * k] = v[k];
-        } else if (ob + 256 * 16 <= n) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (k >= h2) y[ob + 256 * k] = v[k];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (k >= h2 && ob + 256 * k < n) y[ob + 256 * k] = v[k];
+            for (int k = 0; k < 16; ++k) ov[k] = v[k];
+            oseg = seg;
         }
     }
+    if (!(NT & 4) && oseg >= 0) store_out();
+    for (; seg < s1; seg += sstep) boundary(seg);
 }
 
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
@@ -475,40 +333,33 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
     if (!p.interleave) blocks = (nseg + per - 1) / per;
     else if (blocks > nseg) blocks = nseg;
     dim3 grid((unsigned)blocks, (unsigned)channels);
-#define SDSP_OLS_LAUNCH(W, I)                                                                              \
-    hipLaunchKernelGGL((fir_ols4096_kernel<W, I, false>), grid, dim3(256), 0, s, (const cf*)x, (const cf*)hist,      \
+#define SDSP_OLS_LAUNCH(I, NM, H)                                                                                \
+    hipLaunchKernelGGL((fir_ols4096_kernel<I, NM, H, 0>), grid, dim3(256), 0, s, (const cf*)x, (const cf*)hist,      \
                        (const cf*)p.d_H, (const cf*)p.d_tw1, (const cf*)p.d_tw2, (cf*)y, (long long)n, L - 1, h2, \
                        nseg, per)
-#define SDSP_OLS_LAUNCH_D2(I)                                                                              \
-    hipLaunchKernelGGL((fir_ols4096_kernel<false, I, true>), grid, dim3(256), 0, s, (const cf*)x, (const cf*)hist, \
-                       (const cf*)p.d_H, (const cf*)p.d_tw1, (const cf*)p.d_tw2, (cf*)y, (long long)n, L - 1, h2, \
+    if (p.nomem) {  // profiling ablations (h2 = 1 only): 1 no HBM traffic, 2 no loads, 3 no stores
+        if (p.nomem == 2) SDSP_OLS_LAUNCH(true, 2, 1);
+        else if (p.nomem == 3) SDSP_OLS_LAUNCH(true, 3, 1);
+        else SDSP_OLS_LAUNCH(true, 1, 1);
+    } else if (p.interleave && h2 == 1 && p.nt) {
+#define SDSP_OLS_NT(NTV)                                                                                          \
+    hipLaunchKernelGGL((fir_ols4096_kernel<true, 0, 1, NTV>), grid, dim3(256), 0, s, (const cf*)x, (const cf*)hist, \
+                       (const cf*)p.d_H, (const cf*)p.d_tw1, (const cf*)p.d_tw2, (cf*)y, (long long)n, L - 1, h2,  \
                        nseg, per)
-    if (p.occ) {
-        long long ob = (long long)num_cus * p.occ;
-        if (ob > nseg) ob = nseg;
-        dim3 g2((unsigned)ob, (unsigned)channels);
-#define SDSP_OLS_OCC(WV, NM)                                                                                   \
-    hipLaunchKernelGGL((fir_ols4096_occ_kernel<WV, NM>), g2, dim3(256), 0, s, (const cf*)x, (const cf*)hist,      \
-                       (const cf*)p.d_H, (const cf*)p.d_tw1, (const cf*)p.d_tw2, (cf*)y, (long long)n, L - 1, h2, nseg)
-        if (p.occ >= 4) { if (p.nomem) SDSP_OLS_OCC(4, true); else SDSP_OLS_OCC(4, false); }
-        else { if (p.nomem) SDSP_OLS_OCC(3, true); else SDSP_OLS_OCC(3, false); }
-#undef SDSP_OLS_OCC
-    } else if (p.nomem) {
-        hipLaunchKernelGGL((fir_ols4096_kernel<false, true, false, true>), grid, dim3(256), 0, s, (const cf*)x,
-                           (const cf*)hist, (const cf*)p.d_H, (const cf*)p.d_tw1, (const cf*)p.d_tw2, (cf*)y,
-                           (long long)n, L - 1, h2, nseg, per);
-    } else if (p.depth2 && !p.wide) {
-        if (p.interleave) SDSP_OLS_LAUNCH_D2(true);
-        else SDSP_OLS_LAUNCH_D2(false);
-    } else if (p.wide) {
-        if (p.interleave) SDSP_OLS_LAUNCH(true, true);
-        else SDSP_OLS_LAUNCH(true, false);
+        if (p.nt == 1) SDSP_OLS_NT(1);
+        else if (p.nt == 2) SDSP_OLS_NT(2);
+        else if (p.nt == 3) SDSP_OLS_NT(3);
+        else if (p.nt == 4) SDSP_OLS_NT(4);
+        else SDSP_OLS_NT(7);
+#undef SDSP_OLS_NT
+    } else if (p.interleave) {
+        if (h2 == 1) SDSP_OLS_LAUNCH(true, 0, 1);
+        else if (h2 == 2) SDSP_OLS_LAUNCH(true, 0, 2);
+        else SDSP_OLS_LAUNCH(true, 0, 0);
     } else {
-        if (p.interleave) SDSP_OLS_LAUNCH(false, true);
-        else SDSP_OLS_LAUNCH(false, false);
+        SDSP_OLS_LAUNCH(false, 0, 0);
     }
 #undef SDSP_OLS_LAUNCH
-#undef SDSP_OLS_LAUNCH_D2
     return hipGetLastError();
 }
 

@@ -97,7 +97,9 @@ struct sdsp_fir {
     DevBuf stage_in, stage_out;
     // overlap-save plan
     bool ols_ok = false;
-    bool ols_wide = false, ols_interleave = true, ols_depth2 = false, ols_nomem = false;
+    bool ols_wide = false, ols_interleave = true, ols_depth2 = false;
+    int ols_nomem = 0;
+    int ols_nt = 0;
     int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
     int decim_seg = 0;  // outputs per lane group of the polyphase decimator (0 = auto)
     OlsPlan ols{};
@@ -174,6 +176,7 @@ int ols_build(sdsp_fir* h) {
     SDSP_TRY(hipMemcpyAsync(h->d_tw2.p, tw2.data(), tw2.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw2");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     h->ols = OlsPlan{h->d_H.p, h->d_tw1.p, h->d_tw2.p, h2, h->ols_wide, h->ols_interleave, h->ols_depth2, h->ols_nomem, h->ols_occ};
+    h->ols.nt = h->ols_nt;
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -308,11 +311,15 @@ int sdsp_fir_get_algo(const sdsp_fir* h) { return h ? h->algo : -1; }
 int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     switch (key) {
-        case SDSP_TUNE_OLS_WIDE: h->ols_wide = value != 0; break;
+        // retired overlap-save variants (measured slower): only their default is accepted
+        case SDSP_TUNE_OLS_WIDE:
+        case SDSP_TUNE_OLS_DEPTH2:
+        case SDSP_TUNE_OLS_OCCUPANCY:
+            if (value != 0) return SDSP_E_UNSUPPORTED;
+            break;
         case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
-        case SDSP_TUNE_OLS_DEPTH2: h->ols_depth2 = value != 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = value != 0; break;
-        case SDSP_TUNE_OLS_OCCUPANCY: h->ols_occ = (value == 3 || value == 4) ? value : 0; break;
+        case SDSP_TUNE_OLS_NONTEMPORAL: h->ols_nt = value & 7; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 3) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }
@@ -320,6 +327,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     h->ols.interleave = h->ols_interleave;
     h->ols.depth2 = h->ols_depth2;
     h->ols.nomem = h->ols_nomem;
+    h->ols.nt = h->ols_nt;
     h->ols.occ = h->ols_occ;
     return SDSP_OK;
 }

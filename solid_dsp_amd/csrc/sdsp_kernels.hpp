@@ -36,8 +36,9 @@ struct OlsPlan {
     bool wide;        // 16-byte lane-pair global loads/stores
     bool interleave;  // segment order across the persistent grid
     bool depth2;      // two segments of loads in flight (8-byte path)
-    bool nomem;       // profiling ablation: arithmetic only, no HBM traffic (outputs invalid)
-    int occ;          // 0: 2-wave kernel; 3/4: occupancy kernel, blocks per CU
+    int nomem;        // profiling ablation: 1 no HBM traffic, 2 no loads, 3 no stores (outputs invalid)
+    int occ;          // retired (0)
+    int nt = 0;       // nontemporal: bit 0 loads, bit 1 stores
 };
 constexpr int kOlsN = 4096;
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,

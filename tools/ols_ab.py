@@ -24,13 +24,15 @@ def main(rounds=8, log2n=30):
     for cfg in cfgs:
         wide, inter, d2, nomem = cfg[:4]
         occ = cfg[4] if len(cfg) > 4 else 0
+        nt = cfg[5] if len(cfg) > 5 else 0
         f = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, algo=sd.ALGO_FFT)
         sd.lib().sdsp_fir_set_tuning(f._h, 1, wide)
         sd.lib().sdsp_fir_set_tuning(f._h, 2, inter)
         sd.lib().sdsp_fir_set_tuning(f._h, 3, d2)
         sd.lib().sdsp_fir_set_tuning(f._h, 4, nomem)
         sd.lib().sdsp_fir_set_tuning(f._h, 5, occ)
-        variants[f"wide{wide}_inter{inter}_d2{d2}_occ{occ}_nomem{nomem}"] = f
+        sd.lib().sdsp_fir_set_tuning(f._h, 10, nt)
+        variants[f"wide{wide}_inter{inter}_d2{d2}_occ{occ}_nt{nt}_nomem{nomem}"] = f
     s = torch.cuda.current_stream()
     times = {k: [] for k in variants}
     for k, f in variants.items():
