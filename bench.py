@@ -6,7 +6,7 @@ FIR over a 1 GiS synthetic stream per GPU, metric "Msamples/sec 256-tap
 complex FIR @1/2/4/8 GPU; % HBM roofline".  One step = one device-resident
 FIRFilter::execute_block pass (overlap-save kernel) over the whole channel.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--log2n 30] [--algo fft|exact|fma]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1|2|3|4|5] [--log2n 30] [--algo fft|exact|fma]
 
 Other configs (BASELINE.json configs[2..4]):
   3  4-biquad cascade (scipy butter(8, 0.2) SOS), real f32, 1 GiS, block-parallel scan
@@ -38,7 +38,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    p.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
     p.add_argument("--log2n", type=int, default=30, help="samples per GPU per step (configs 2-4)")
     p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"], help="config 2 kernel")
     p.add_argument("--cpu-samples", type=int, default=None,
@@ -63,15 +63,48 @@ def load_traffic(config, log2n, algo):
     return None
 
 
-def timed_cpu(run_chunk, label, samples, chunk, cores=1):
-    """Stream `samples` inputs through one CPU filter object, `chunk` at a time
-    (the same synthetic chunk re-fed, so host memory stays bounded)."""
-    reps = max(1, samples // chunk)
-    t0 = time.perf_counter()
+def stream_copy_gbps(torch, sd, nbytes=4 << 30, reps=5):
+    """Achievable HBM bandwidth on this box: one-shot 16-byte-per-lane device copy
+    (read + write bytes / time, median of `reps`), measured in the same run."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    st = torch.cuda.current_stream()
+    L = sd.lib()
+    L.sdsp_bandwidth_copy_device(a.data_ptr(), b.data_ptr(), nbytes, st.cuda_stream)
+    ts = []
     for _ in range(reps):
-        run_chunk()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        L.sdsp_bandwidth_copy_device(a.data_ptr(), b.data_ptr(), nbytes, st.cuda_stream)
+        e1.record(st)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    del a, b
+    torch.cuda.empty_cache()
+    return 2.0 * nbytes / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e9
+
+
+def timed_cpu(run_chunk, label, samples, chunk, cores=1):
+    """Stream `samples` inputs through CPU filter objects, `chunk` at a time (the
+    same synthetic chunk re-fed, so host memory stays bounded).  cores > 1: one
+    independent channel per thread (the restatement is C; ctypes releases the GIL),
+    each thread streaming samples / cores."""
+    reps = max(1, samples // (chunk * cores))
+    t0 = time.perf_counter()
+    if cores == 1:
+        for _ in range(reps):
+            run_chunk(0)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+
+        def worker(c):
+            for _ in range(reps):
+                run_chunk(c)
+        with ThreadPoolExecutor(cores) as ex:
+            list(ex.map(worker, range(cores)))
     dt = time.perf_counter() - t0
-    total = reps * chunk
+    total = reps * chunk * cores
     return {"value": total / dt / 1e6, "unit": "Msamples/sec", "cores": cores, "kind": "port",
             "sample": f"{label}; {total} input samples streamed in {reps} execute_block calls of {chunk}, "
                       f"{cores} thread(s), {dt:.1f} s"}
@@ -128,7 +161,7 @@ class Cfg2FIR:
         import oracle_lib as O
         x = O.synth(SEED, 0, 0, CPU_CHUNK, complex_=True).astype(np.complex128)
         f = O.fir(O.RC64, self.h.astype(np.float64), 0.2)
-        return timed_cpu(lambda: f.execute_block(x), "FIRFilter<f64, Complex<f64>> restatement (memmove Window + "
+        return timed_cpu(lambda c: f.execute_block(x), "FIRFilter<f64, Complex<f64>> restatement (memmove Window + "
                          "to_vec + sequential dot)", samples, CPU_CHUNK)
 
 
@@ -176,7 +209,8 @@ class Cfg3IIR:
         import oracle_lib as O
         x = O.synth(SEED, 0, 0, CPU_CHUNK).astype(np.float64)
         f = O.iir(O.RR64, self.ff.astype(np.float64), self.fb.astype(np.float64), O.SECOND_ORDER)
-        return timed_cpu(lambda: f.execute_block(x), "IIRFilter<f64, f64> SecondOrder restatement", samples, CPU_CHUNK)
+        return timed_cpu(lambda c: f.execute_block(x), "IIRFilter<f64, f64> SecondOrder restatement", samples,
+                         CPU_CHUNK)
 
 
 class Cfg4Decim:
@@ -228,8 +262,8 @@ class Cfg4Decim:
         import oracle_lib as O
         x = O.synth(SEED, 0, 0, CPU_CHUNK, complex_=True).astype(np.complex128)
         f = O.decim(O.RC64, self.h.astype(np.float64), 1.0 / 32, 32)
-        return timed_cpu(lambda: f.execute_block(x), "DecimatingFIRFilter<f64, Complex<f64>> restatement", samples,
-                         CPU_CHUNK)
+        return timed_cpu(lambda c: f.execute_block(x), "DecimatingFIRFilter<f64, Complex<f64>> restatement",
+                         samples, CPU_CHUNK)
 
 
 class Cfg5Chan:
@@ -274,19 +308,71 @@ class Cfg5Chan:
         return float(np.linalg.norm(y - ref) / np.linalg.norm(ref))
 
     def cpu(self, samples):
+        """8 streams on min(8, host cores) threads, one stream per thread."""
         import oracle_lib as O
         chunk = CPU_CHUNK // self.M * self.M
-        x = O.synth(SEED, 0, 0, chunk, complex_=True).astype(np.complex128)
-        out = np.zeros(chunk, np.complex128)
+        cores = max(1, min(self.S, os.cpu_count() or 1))
+        xs = [O.synth(SEED, c, 0, chunk, complex_=True).astype(np.complex128) for c in range(cores)]
+        outs = [np.zeros(chunk, np.complex128) for _ in range(cores)]
         h = self.h.astype(np.float64)
         # each call is a fresh channeliser over the chunk (the restatement has no carried state)
-        return timed_cpu(lambda: O.lib().orc_channelize(O._ptr(h), len(h), self.M, O._ptr(x), chunk, O._ptr(out)),
-                         "channeliser restatement (PFB DotProducts + reference mixed-radix FFT)", samples, chunk)
+        return timed_cpu(lambda c: O.lib().orc_channelize(O._ptr(h), len(h), self.M, O._ptr(xs[c]), chunk,
+                                                          O._ptr(outs[c])),
+                         "channeliser restatement (PFB DotProducts + reference mixed-radix FFT)", samples, chunk,
+                         cores)
 
 
-WORKLOADS = {2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan}
+class Cfg1FIR:
+    """cfg1 plumbing case: 63-tap real f32 FIR, firdes_kaiser(63, 0.2, 60), 2^20 samples,
+    reference-order EXACT kernel (bit-identical to the f32 restatement)."""
+    metric = "Msamples/sec 63-tap real-f32 FIR, 1 MiS (plumbing case)"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import FIRFilter
+        from solid_dsp_amd.filter import firdes
+        self.n = 1 << 20
+        self.h = firdes.firdes_kaiser(63, 0.2, 60.0, 0.0).astype(np.float32)
+        self.f = FIRFilter(self.h, np.float32(1.0), sample_dtype=np.float32, device=dev, algo=sd.ALGO_EXACT)
+        self.d_in = torch.empty(self.n, dtype=torch.float32, device="cuda")
+        self.d_out = torch.empty(self.n, dtype=torch.float32, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        self.bytes_per_step = 8 * self.n
+        self.dtype = "f32 (f32 taps x real f32 samples, reference summation order)"
+        self.kernel = "fir_direct_kernel<EXACT>"
+        self.parity_check = "bit mismatches vs the f32 restatement, whole stream (must be 0)"
+        self.workload = "cfg1: 63-tap real f32 FIR, firdes_kaiser(63, 0.2, 60), 2^20 samples"
+        self.algo_name = "exact"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng):
+        """bit-exact against the f32 restatement over the whole stream (fresh handle)"""
+        import oracle_lib as O
+        import torch
+        from solid_dsp_amd import FIRFilter
+        import solid_dsp_amd as sd
+        g = FIRFilter(self.h, np.float32(1.0), sample_dtype=np.float32, algo=sd.ALGO_EXACT)
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        x = self.d_in.cpu().numpy()
+        y = self.d_out.cpu().numpy()
+        ref = O.fir(O.RR32, self.h, np.float32(1.0)).execute_block(x)
+        return float(np.count_nonzero(y.view(np.uint32) != ref.view(np.uint32)))
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = O.synth(SEED, 0, 0, CPU_CHUNK).astype(np.float64)
+        f = O.fir(O.RR64, self.h.astype(np.float64), 1.0)
+        return timed_cpu(lambda c: f.execute_block(x), "FIRFilter<f64, f64> restatement (memmove Window + to_vec + "
+                         "sequential dot)", samples, CPU_CHUNK)
+
+
+WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan}
 # bounded CPU samples: about 10-20 s of single-thread work each on a current x86 host
-CPU_DEFAULT = {2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 29}
+CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32}
 CPU_CHUNK = 1 << 22
 
 
@@ -352,6 +438,7 @@ def main():
         value = world * w.samples_per_step * args.steps / wall / 1e6
         kern_ms = float(np.mean(ev_ms))
         achieved = w.bytes_per_step / (kern_ms * 1e-3) / 1e9
+        stream = stream_copy_gbps(torch, sd)
         out = {
             "metric": w.metric,
             "value": round(value, 1),
@@ -370,8 +457,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(args.config, args.log2n, w.algo_name),
-                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": w.bytes_per_step},
-            "parity_rel_rms_vs_f64_oracle": parity,
+                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": w.bytes_per_step,
+                         "stream_copy_GBps": round(stream, 1), "frac_of_stream_copy": round(achieved / stream, 4)},
+            "parity": {"check": getattr(w, "parity_check", "rel_rms vs the f64 restatement (tolerance 1e-6, IIR 1e-5)"),
+                       "value": parity},
             "gather_ms": gather_ms,
         }
         if not args.no_cpu:
