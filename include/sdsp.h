@@ -128,7 +128,8 @@ typedef enum {
                                     2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */
     SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: 1 (default) = streaming M=1024 kernel where it applies, 0 = per-frame */
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
-    SDSP_TUNE_OLS_NONTEMPORAL = 10  /* overlap-save streaming loads (bit 0) / stores (bit 1) */
+    SDSP_TUNE_OLS_NONTEMPORAL = 10, /* overlap-save streaming loads (bit 0) / stores (bit 1) */
+    SDSP_TUNE_OLS_WAVE = 11         /* overlap-save: 1 = wave-per-segment N=1024 kernel (L <= 257) */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */

@@ -106,6 +106,13 @@ constexpr int kRegion = 16 * kRowA;  // samples per LDS region
 // B image: 256 rows x 16 samples, pairs XOR-swizzled by (row>>1)&7
 __device__ __forceinline__ int bidx(int r, int c) { return r * 16 + ((((c >> 1) ^ (r >> 1)) & 7) << 1) + (c & 1); }
 
+// LDS hand-off between the lanes of one wave (LDS counter only; global loads
+// and stores stay in flight)
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <bool CHECK>
 __device__ __forceinline__ cf ext_ld(const cf* __restrict__ x, const cf* __restrict__ hist, long long j, long long n,
                                      int Lm1) {
@@ -321,6 +328,155 @@ fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const 
     for (; seg < s1; seg += sstep) boundary(seg);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-per-segment overlap-save, N = 1024 (`SDSP_TUNE_OLS_WAVE`).  Each wave
+// owns whole segments, 16 points per lane, and transposes only through its
+// own LDS buffer, so a segment needs no workgroup barrier:
+//     n = n0 + 4 n1 + 64 n2,  k = k2 + 16 k1 + 256 k0
+//   P1  lane L = n0 + 4 n1: DFT16 n2 -> k2, * W1024^(L k2)      -> LDS rows n0 + 4 k2
+//   P2  lane (n0, k2):      DFT16 n1 -> k1, * W1024^(16 n0 k1)   -> LDS [k2 + 16 k1][n0]
+//   P3  lane l, c = l + 64 j: DFT4 n0 -> k0, * H[c + 256 k0] (natural order, /N, scale),
+//                           IDFT4 k0 -> n0                    -> LDS [c][n0]
+//   P2' lane (n0, k2):      * W1024^-(16 n0 k1), IDFT16 k1 -> n1 -> LDS rows
+//   P1' lane (n0, n1):      * W1024^-(L k2), IDFT16 k2 -> n2, store rows n2 >= HR
+// The halo is HR rows of 64 samples (64 HR >= L - 1); a segment yields 1024 - 64 HR
+// outputs.  A 1024-thread workgroup shares the twiddle and spectrum tables in
+// LDS, one 8.7 KB transpose buffer per wave (rows of 17: 16 lanes reading the
+// same slot of consecutive rows hit distinct banks).
+constexpr int kWRow = 17;
+constexpr int kWBuf = 64 * kWRow;
+
+template <int HR, int NOMEM>
+__global__ void __launch_bounds__(1024)
+fir_ols1024_wave_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const cf* __restrict__ H1k,
+                        const cf* __restrict__ tw1k, cf* __restrict__ y, long long n, int Lm1, long long nseg) {
+    __shared__ cf sTw[1024];
+    __shared__ cf sH[1024];
+    __shared__ cf sBuf[16 * kWBuf];
+    const int tid = threadIdx.x, L = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    for (int i = tid; i < 1024; i += 1024) {
+        sTw[i] = tw1k[i];
+        sH[i] = H1k[i];
+    }
+    __syncthreads();
+    const int ch = blockIdx.y;
+    x += (long long)ch * n;
+    y += (long long)ch * n;
+    hist += (long long)ch * Lm1;
+    cf* const buf = sBuf + wv * kWBuf;
+    constexpr int V = 1024 - 64 * HR;
+    const int n0 = L & 3, n1 = L >> 2;  // P1 / P1' view
+    const int k2v = L >> 2;             // P2 / P2' view: lane = n0 + 4 k2
+
+    const long long gw = (long long)blockIdx.x * 16 + wv;
+    const long long GW = (long long)gridDim.x * 16;
+    auto base_of = [&](long long sg) { return sg * V - 64 * HR; };
+    auto interior = [&](long long sg) { return sg < nseg && base_of(sg) >= 0 && base_of(sg) + 1024 <= n; };
+
+    auto segment = [&](cf (&v)[16], auto&& after_p1) {
+        // P1
+        dft16<false>(v);
+#pragma unroll
+        for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], sTw[(L * k) & 1023]);
+        after_p1();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) buf[(n0 + 4 * k) * kWRow + n1] = v[k];
+        wave_sync_lds();
+        // P2
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = buf[L * kWRow + i];
+        dft16<false>(v);
+#pragma unroll
+        for (int k = 1; k < 16; ++k) v[k] = cmul(v[k], sTw[(16 * n0 * k) & 1023]);
+        wave_sync_lds();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) buf[(k2v + 16 * k) * 4 + n0] = v[k];
+        wave_sync_lds();
+        // P3: DFT4, spectrum, IDFT4 per column c
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int c = L + 64 * j;
+            cf a0 = buf[c * 4 + 0], a1 = buf[c * 4 + 1], a2 = buf[c * 4 + 2], a3 = buf[c * 4 + 3];
+            dft4<false>(a0, a1, a2, a3);
+            a0 = cmul(a0, sH[c]);
+            a1 = cmul(a1, sH[c + 256]);
+            a2 = cmul(a2, sH[c + 512]);
+            a3 = cmul(a3, sH[c + 768]);
+            dft4<true>(a0, a1, a2, a3);
+            buf[c * 4 + 0] = a0;
+            buf[c * 4 + 1] = a1;
+            buf[c * 4 + 2] = a2;
+            buf[c * 4 + 3] = a3;
+        }
+        wave_sync_lds();
+        // P2'
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = buf[(k2v + 16 * k) * 4 + n0];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) v[k] = cmulc(v[k], sTw[(16 * n0 * k) & 1023]);
+        dft16<true>(v);
+        wave_sync_lds();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) buf[L * kWRow + i] = v[i];
+        wave_sync_lds();
+        // P1'
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = buf[(n0 + 4 * k) * kWRow + n1];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) v[k] = cmulc(v[k], sTw[(L * k) & 1023]);
+        dft16<true>(v);
+        wave_sync_lds();  // buffer free for the next segment
+    };
+
+    // boundary segments: guarded element loads and stores
+    auto boundary = [&](long long sg) {
+        cf v[16];
+        const long long base = base_of(sg);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = ext_ld<true>(x, hist, base + L + 64 * r, n, Lm1);
+        segment(v, [] {});
+#pragma unroll
+        for (int r = HR; r < 16; ++r)
+            if (base + L + 64 * r < n) y[base + L + 64 * r] = v[r];
+    };
+
+    long long seg = gw;
+    if (seg < nseg && !interior(seg)) {
+        boundary(seg);
+        seg += GW;
+    }
+    cf nv[16];
+    auto load = [&](long long sg) {
+        if constexpr (NOMEM) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) nv[r] = cf{(float)(L + r), (float)(sg & 1023)};
+        } else {
+            const cf* xb = x + base_of(sg) + L;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) nv[r] = xb[64 * r];
+        }
+    };
+    if (interior(seg)) load(seg);
+    for (; interior(seg); seg += GW) {
+        cf v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = nv[r];
+        const long long nxt = interior(seg + GW) ? seg + GW : seg;
+        segment(v, [&] { load(nxt); });
+        cf* yb = y + base_of(seg) + L;
+        if constexpr (NOMEM) {
+#pragma unroll
+            for (int r = HR; r < 16; ++r)
+                if (v[r].re == 1234.5678f) yb[64 * r] = v[r];
+        } else {
+#pragma unroll
+            for (int r = HR; r < 16; ++r) yb[64 * r] = v[r];
+        }
+    }
+    for (; seg < nseg; seg += GW) boundary(seg);
+}
+
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
                           size_t channels, int num_cus, hipStream_t s) {
     if (n == 0) return hipSuccess;
@@ -337,6 +493,29 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
     hipLaunchKernelGGL((fir_ols4096_kernel<I, NM, H, 0>), grid, dim3(256), 0, s, (const cf*)x, (const cf*)hist,      \
                        (const cf*)p.d_H, (const cf*)p.d_tw1, (const cf*)p.d_tw2, (cf*)y, (long long)n, L - 1, h2, \
                        nseg, per)
+    if (p.wave && p.d_H1k) {
+        const int hr = p.halo_rows_1k;
+        const long long V1 = 1024 - 64 * hr;
+        const long long nseg1 = ((long long)n + V1 - 1) / V1;
+        long long wg = ((nseg1 + 15) / 16 + 3) / 4;  // about four segments per wave
+        const long long cap = (long long)num_cus * 8;
+        if (wg > cap) wg = cap;
+        if (wg < 1) wg = 1;
+        dim3 g1((unsigned)wg, (unsigned)channels);
+#define SDSP_OLS_WAVE(HRV, NM)                                                                                   \
+    hipLaunchKernelGGL((fir_ols1024_wave_kernel<HRV, NM>), g1, dim3(1024), 0, s, (const cf*)x, (const cf*)hist,   \
+                       (const cf*)p.d_H1k, (const cf*)p.d_tw1k, (cf*)y, (long long)n, L - 1, nseg1)
+        const int nm = p.nomem == 1 ? 1 : 0;
+        switch (hr) {
+            case 1: if (nm) SDSP_OLS_WAVE(1, 1); else SDSP_OLS_WAVE(1, 0); break;
+            case 2: if (nm) SDSP_OLS_WAVE(2, 1); else SDSP_OLS_WAVE(2, 0); break;
+            case 3: if (nm) SDSP_OLS_WAVE(3, 1); else SDSP_OLS_WAVE(3, 0); break;
+            case 4: if (nm) SDSP_OLS_WAVE(4, 1); else SDSP_OLS_WAVE(4, 0); break;
+            default: return hipErrorInvalidValue;
+        }
+#undef SDSP_OLS_WAVE
+        return hipGetLastError();
+    }
     if (p.nomem) {  // profiling ablations (h2 = 1 only): 1 no HBM traffic, 2 no loads, 3 no stores
         if (p.nomem == 2) SDSP_OLS_LAUNCH(true, 2, 1);
         else if (p.nomem == 3) SDSP_OLS_LAUNCH(true, 3, 1);

@@ -100,7 +100,7 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
     return v;
 }
 
-template <int S, typename C, typename I, int CB>
+template <int S, typename C, typename I, int CB, bool RERUN>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
@@ -195,7 +195,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 __builtin_memcpy(e, &val, 16);
 #pragma unroll
                 for (int i = 0; i < E; ++i) e[i] = sos_step_f<S>(coefs, e[i], w1, w2);
-                *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
+                if constexpr (!RERUN) *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
             }
 #pragma unroll
             for (int q = 0; q < S; ++q) { s[2 * q] = w1[q]; s[2 * q + 1] = w2[q]; }
@@ -234,19 +234,35 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 #pragma unroll
         for (int d = 0; d < D; ++d) carry[d] = readlane_v(s[d], 63);
 
-        // 4. correction by the state response
+        // 4. outputs: correction by the state response (y0 in place), or (RERUN) the
+        //    chunk rerun from its true initial state over the staged input
+        if constexpr (RERUN) {
+            I w1[S], w2[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) { w1[q] = init[2 * q]; w2[q] = init[2 * q + 1]; }
 #pragma unroll 2
-        for (int o = 0; o < kVecPerRow; ++o) {
-            I e[E];
-            const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
-            __builtin_memcpy(e, &val, 16);
+            for (int o = 0; o < kVecPerRow; ++o) {
+                I e[E];
+                const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
+                __builtin_memcpy(e, &val, 16);
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                const C* cr = sCr + (o * E + i) * D;
-#pragma unroll
-                for (int d = 0; d < D; ++d) e[i] = fmac_(e[i], cr[d], init[d]);
+                for (int i = 0; i < E; ++i) e[i] = sos_step_f<S>(coefs, e[i], w1, w2);
+                *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
             }
-            *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
+        } else {
+#pragma unroll 2
+            for (int o = 0; o < kVecPerRow; ++o) {
+                I e[E];
+                const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
+                __builtin_memcpy(e, &val, 16);
+#pragma unroll
+                for (int i = 0; i < E; ++i) {
+                    const C* cr = sCr + (o * E + i) * D;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) e[i] = fmac_(e[i], cr[d], init[d]);
+                }
+                *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
+            }
         }
 
         // exact final state: the lane of this segment holding sample nd-1 reruns its chunk
@@ -577,7 +593,7 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-template <typename C, typename I, int S, int CB>
+template <typename C, typename I, int S, int CB, bool RERUN>
 hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     constexpr int B = ws_chunk<I, CB>::B;
     const long long nd = (long long)a.n;
@@ -592,23 +608,23 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
                         (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
     const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * 4 * S * S + B * 2 * S);
-    hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
+    hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
                        tpw, vec_ok);
     return hipGetLastError();
 }
 
-template <typename C, typename I, int CB>
+template <typename C, typename I, int CB, bool RERUN = false>
 hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
     switch (a.sections) {
-        case 1: return launch_wscan_t<C, I, 1, CB>(a, st);
-        case 2: return launch_wscan_t<C, I, 2, CB>(a, st);
-        case 3: return launch_wscan_t<C, I, 3, CB>(a, st);
-        case 4: return launch_wscan_t<C, I, 4, CB>(a, st);
-        case 5: return launch_wscan_t<C, I, 5, CB>(a, st);
-        case 6: return launch_wscan_t<C, I, 6, CB>(a, st);
-        case 7: return launch_wscan_t<C, I, 7, CB>(a, st);
-        case 8: return launch_wscan_t<C, I, 8, CB>(a, st);
+        case 1: return launch_wscan_t<C, I, 1, CB, RERUN>(a, st);
+        case 2: return launch_wscan_t<C, I, 2, CB, RERUN>(a, st);
+        case 3: return launch_wscan_t<C, I, 3, CB, RERUN>(a, st);
+        case 4: return launch_wscan_t<C, I, 4, CB, RERUN>(a, st);
+        case 5: return launch_wscan_t<C, I, 5, CB, RERUN>(a, st);
+        case 6: return launch_wscan_t<C, I, 6, CB, RERUN>(a, st);
+        case 7: return launch_wscan_t<C, I, 7, CB, RERUN>(a, st);
+        case 8: return launch_wscan_t<C, I, 8, CB, RERUN>(a, st);
     }
     return hipErrorInvalidValue;
 }
@@ -619,15 +635,17 @@ hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
         if (a.ws_variant == 2) return launch_wscan2_s<128>(a, st);
         if (a.ws_variant == 3) return launch_wscan2_s<64>(a, st);
     }
+    if (a.ws_variant == 4) return launch_wscan_s<C, I, 256, true>(a, st);  // rerun instead of correction
     return a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st) : launch_wscan_s<C, I, 256>(a, st);
 }
 
 }  // namespace
 
 int iir_wscan_chunk(int dtype, int variant) {
-    // variants: 0 = 256-byte chunks, 1 = 128-byte, 2/3 = paired 128/64-byte chunks (real f32 only)
-    if (variant >= 2 && dtype != 0) return 0;
-    const int cb = variant == 0 ? 256 : (variant == 3 ? 64 : 128);
+    // variants: 0 = 256-byte chunks, 1 = 128-byte, 2/3 = paired 128/64-byte chunks (real f32 only),
+    // 4 = 256-byte chunks with a rerun instead of the state-response correction
+    if ((variant == 2 || variant == 3) && dtype != 0) return 0;
+    const int cb = (variant == 0 || variant == 4) ? 256 : (variant == 3 ? 64 : 128);
     switch (dtype) {
         case 0: return cb / (int)sizeof(float);
         case 1: return cb / (int)sizeof(c32);

@@ -103,7 +103,8 @@ struct sdsp_fir {
     int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
     int decim_seg = 0;  // outputs per lane group of the polyphase decimator (0 = auto)
     OlsPlan ols{};
-    DevBuf d_H, d_tw1, d_tw2;
+    DevBuf d_H, d_tw1, d_tw2, d_H1k, d_tw1k;
+    bool ols_wave = false;  // wave-per-segment N = 1024 kernel (SDSP_TUNE_OLS_WAVE)
 };
 
 namespace {
@@ -174,9 +175,39 @@ int ols_build(sdsp_fir* h) {
     SDSP_TRY(hipMemcpyAsync(h->d_H.p, Hs.data(), Hs.size() * 4, hipMemcpyHostToDevice, h->stream), "copy H");
     SDSP_TRY(hipMemcpyAsync(h->d_tw1.p, tw1.data(), tw1.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw1");
     SDSP_TRY(hipMemcpyAsync(h->d_tw2.p, tw2.data(), tw2.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw2");
+    // N = 1024 natural-order spectrum and twiddles for the wave-per-segment kernel (L - 1 <= 256)
+    int hr1k = 0;
+    if (L - 1 <= 256) {
+        hr1k = (int)((L - 1 + 63) / 64);
+        if (hr1k < 1) hr1k = 1;
+        std::vector<float> H1(2 * 1024), T1(2 * 1024);
+        const double w1 = -2.0 * M_PI / 1024.0;
+        for (int k = 0; k < 1024; ++k) {
+            double re = 0.0, im = 0.0;
+            for (size_t i = 0; i < L; ++i) {
+                const long long ph = ((long long)i * k) % 1024;
+                const double c = std::cos(w1 * (double)ph), sn = std::sin(w1 * (double)ph);
+                re += g[i].re * c - g[i].im * sn;
+                im += g[i].re * sn + g[i].im * c;
+            }
+            H1[2 * k] = (float)(re / 1024.0);
+            H1[2 * k + 1] = (float)(im / 1024.0);
+            T1[2 * k] = (float)std::cos(w1 * k);
+            T1[2 * k + 1] = (float)std::sin(w1 * k);
+        }
+        SDSP_TRY(h->d_H1k.ensure(H1.size() * 4), "alloc H1k");
+        SDSP_TRY(h->d_tw1k.ensure(T1.size() * 4), "alloc tw1k");
+        SDSP_TRY(hipMemcpyAsync(h->d_H1k.p, H1.data(), H1.size() * 4, hipMemcpyHostToDevice, h->stream), "copy H1k");
+        SDSP_TRY(hipMemcpyAsync(h->d_tw1k.p, T1.data(), T1.size() * 4, hipMemcpyHostToDevice, h->stream),
+                 "copy tw1k");
+    }
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     h->ols = OlsPlan{h->d_H.p, h->d_tw1.p, h->d_tw2.p, h2, h->ols_wide, h->ols_interleave, h->ols_depth2, h->ols_nomem, h->ols_occ};
     h->ols.nt = h->ols_nt;
+    h->ols.d_H1k = hr1k ? h->d_H1k.p : nullptr;
+    h->ols.d_tw1k = hr1k ? h->d_tw1k.p : nullptr;
+    h->ols.halo_rows_1k = hr1k;
+    h->ols.wave = h->ols_wave && hr1k > 0;
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -285,6 +316,8 @@ void sdsp_fir_destroy(sdsp_fir* h) {
         h->d_H.release();
         h->d_tw1.release();
         h->d_tw2.release();
+        h->d_H1k.release();
+        h->d_tw1k.release();
     }
     delete h;
 }
@@ -319,6 +352,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
             break;
         case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
         case SDSP_TUNE_OLS_NONTEMPORAL: h->ols_nt = value & 7; break;
+        case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
         case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 3) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
@@ -329,6 +363,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     h->ols.nomem = h->ols_nomem;
     h->ols.nt = h->ols_nt;
     h->ols.occ = h->ols_occ;
+    h->ols.wave = h->ols_wave && h->ols.halo_rows_1k > 0;
     return SDSP_OK;
 }
 

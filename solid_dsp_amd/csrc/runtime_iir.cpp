@@ -37,7 +37,7 @@ struct Group {
     struct WaveScan {          // wave-scan tables per chunk-size variant (256 B, 128 B)
         int wc = 0;
         DevBuf d_P, d_Cr;      // [6][2c][2c], [B][2c] output response to the state
-    } ws[4];
+    } ws[5];
 };
 
 struct DeviceGuardI {
@@ -225,7 +225,7 @@ int plan_groups(sdsp_iir* h) {
         if (st) return st;
         if (g.wc == 0) continue;
         // wave scan (kern_iir_wscan.hip), one table set per chunk size: 6 powers, warm-up <= 32 chunks
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < 5; ++v) {
             const int Bw = iir_wscan_chunk(h->dtype, v);
             if (Bw == 0) continue;
             st = scan_tables(h, g, Bw, 32, 7, &g.ws[v].wc, &g.ws[v].d_P, &g.ws[v].d_Cr);
@@ -426,7 +426,7 @@ int sdsp_iir_set_algo(sdsp_iir* h, int algo) {
 int sdsp_iir_set_tuning(sdsp_iir* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (key != SDSP_TUNE_IIR_WAVE_SCAN) return SDSP_E_INVALID_ARGUMENT;
-    if (value < 0 || value > 4) return SDSP_E_INVALID_ARGUMENT;
+    if (value < 0 || value > 5) return SDSP_E_INVALID_ARGUMENT;
     h->wscan = value;
     return SDSP_OK;
 }

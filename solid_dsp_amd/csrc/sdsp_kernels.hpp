@@ -39,6 +39,11 @@ struct OlsPlan {
     int nomem;        // profiling ablation: 1 no HBM traffic, 2 no loads, 3 no stores (outputs invalid)
     int occ;          // retired (0)
     int nt = 0;       // nontemporal: bit 0 loads, bit 1 stores
+    // wave-per-segment N = 1024 kernel (L - 1 <= 256)
+    void* d_H1k = nullptr;   // [1024] c32: natural-order spectrum / 1024 * scale
+    void* d_tw1k = nullptr;  // [1024] c32: W1024^m
+    int halo_rows_1k = 0;    // HR: 64 HR >= L - 1
+    bool wave = false;
 };
 constexpr int kOlsN = 4096;
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,

@@ -131,6 +131,24 @@ def test_fir_fft_tolerance(dt, cdt, L):
     assert np.abs(y - ref).max() <= bound
 
 
+@pytest.mark.parametrize("dt,cdt", [(O.RC32, F32), (O.CC32, C64)])
+@pytest.mark.parametrize("L", [2, 64, 200, 256, 257])
+def test_fir_fft_wave_kernel_tolerance(dt, cdt, L):
+    # wave-per-segment N=1024 overlap-save (SDSP_TUNE_OLS_WAVE = 11): ragged calls, vs f64 restatement
+    h = _f32_taps(L, 0.1)
+    if cdt == C64:
+        h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
+    x = O.synth(20250226, 2, 0, 400000, complex_=True)
+    f = FIRFilter(h, cdt(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    assert sd.lib().sdsp_fir_set_tuning(f._h, 11, 1) == 0
+    cuts = [0, 1, 1000, 70001, 300007, 400000]
+    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
+    ref = O.fir(O.CC64, h.astype(C128), 0.2 + 0j).execute_block(x.astype(C128))
+    assert rel_rms(y, ref) <= 1e-6
+    bound = 1e-6 * np.abs(h).sum() * 0.2 * np.abs(x).max()
+    assert np.abs(y - ref).max() <= bound
+
+
 def test_fir_fft_matches_exact_kernel_across_calls():
     h = _f32_taps(256, 0.1)
     x = O.synth(7, 3, 0, 200000, complex_=True)

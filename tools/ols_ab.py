@@ -25,6 +25,7 @@ def main(rounds=8, log2n=30):
         wide, inter, d2, nomem = cfg[:4]
         occ = cfg[4] if len(cfg) > 4 else 0
         nt = cfg[5] if len(cfg) > 5 else 0
+        wave = cfg[6] if len(cfg) > 6 else 0
         f = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, algo=sd.ALGO_FFT)
         sd.lib().sdsp_fir_set_tuning(f._h, 1, wide)
         sd.lib().sdsp_fir_set_tuning(f._h, 2, inter)
@@ -32,7 +33,8 @@ def main(rounds=8, log2n=30):
         sd.lib().sdsp_fir_set_tuning(f._h, 4, nomem)
         sd.lib().sdsp_fir_set_tuning(f._h, 5, occ)
         sd.lib().sdsp_fir_set_tuning(f._h, 10, nt)
-        variants[f"wide{wide}_inter{inter}_d2{d2}_occ{occ}_nt{nt}_nomem{nomem}"] = f
+        sd.lib().sdsp_fir_set_tuning(f._h, 11, wave)
+        variants[f"wave{wave}_inter{inter}_nt{nt}_nomem{nomem}"] = f
     s = torch.cuda.current_stream()
     times = {k: [] for k in variants}
     for k, f in variants.items():
@@ -42,8 +44,14 @@ def main(rounds=8, log2n=30):
         outs[k] = o[: 1 << 22].cpu().numpy().copy(), o[-(1 << 20):].cpu().numpy().copy()
         del o
     ref = outs[next(k for k in outs if k.endswith("nomem0"))]
-    same = {k: bool(np.array_equal(v[0].view(np.uint64), ref[0].view(np.uint64)) and
-                    np.array_equal(v[1].view(np.uint64), ref[1].view(np.uint64))) for k, v in outs.items()}
+
+    def agree(v):  # bit-identical within a kernel family; wave kernel (N=1024) differs in rounding only
+        if np.array_equal(v[0].view(np.uint64), ref[0].view(np.uint64)):
+            return True
+        a = np.concatenate([v[0], v[1]]).astype(np.complex128)
+        b = np.concatenate([ref[0], ref[1]]).astype(np.complex128)
+        return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+    same = {k: agree(v) for k, v in outs.items()}
     d_out = torch.empty_like(d_in)
     for r in range(rounds):
         for k, f in variants.items():
