@@ -132,24 +132,30 @@ __device__ __forceinline__ cf ext_ld(const cf* __restrict__ x, const cf* __restr
 // P1..P5 of one segment on v (loaded: lane t holds x over n2).  `after_p1` runs
 // right after P1's LDS writes (the next segment's loads go out there).  On return
 // v holds the segment's outputs over rows n2.
-template <typename F>
+// NOBAR: profiling ablation only (wrong results): the four barriers become
+// wave barriers, to price workgroup synchronisation
+template <bool NOBAR = false, typename F>
 __device__ __forceinline__ void ols_segment(cf (&v)[16], cf* __restrict__ rA, cf* __restrict__ rB,
                                             const cf (&w1)[16], const cf (&w2)[16], const cf (&Hr)[16], int t,
                                             F&& after_p1) {
     const int hi4 = t >> 4, lo4 = t & 15;
+    auto bar = [] {
+        if constexpr (NOBAR) __builtin_amdgcn_wave_barrier();
+        else __syncthreads();
+    };
     // P1: DFT over n2 -> k0, twiddle, A[k0][t]
     dft16<false>(v);
 #pragma unroll
     for (int k = 0; k < 16; ++k) rA[k * kRowA + t] = cmul(v[k], w1[k]);
     after_p1();
-    __syncthreads();
+    bar();
     // P2: lane (k0=hi4, n0=lo4) reads n1
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = rA[hi4 * kRowA + 16 * k + lo4];
     dft16<false>(v);
 #pragma unroll
     for (int k = 0; k < 16; ++k) rB[bidx(16 * hi4 + k, lo4)] = cmul(v[k], w2[k]);
-    __syncthreads();
+    bar();
     // P3: lane (k0=hi4, k1=lo4) reads its row over n0
     {
         const float4* row = reinterpret_cast<const float4*>(rB + t * 16);
@@ -174,14 +180,14 @@ __device__ __forceinline__ void ols_segment(cf (&v)[16], cf* __restrict__ rA, cf
             row[(p ^ (t >> 1)) & 7] = make_float4(a.re, a.im, b.re, b.im);
         }
     }
-    __syncthreads();
+    bar();
     // P4: lane (k0=hi4, n0=lo4) reads k1
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = rA[bidx(16 * hi4 + k, lo4)];
     dft16<true>(v);
 #pragma unroll
     for (int k = 0; k < 16; ++k) rB[hi4 * kRowA + 16 * k + lo4] = v[k];
-    __syncthreads();
+    bar();
     // P5: lane t=(n1,n0) reads k0
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = cmulc(rB[k * kRowA + t], w1[k]);
@@ -264,7 +270,7 @@ fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const 
     }
     cf nv[16];
     auto load = [&](long long sg) {
-        if constexpr (ABL == 1 || ABL == 2) {  // ablation builds: no input traffic, same arithmetic
+        if constexpr (ABL == 1 || ABL == 2 || ABL == 4) {  // ablation builds: no input traffic, same arithmetic
 #pragma unroll
             for (int r = 0; r < 16; ++r) nv[r] = cf{(float)(t + r), (float)(sg & 1023)};
         } else {
@@ -287,7 +293,7 @@ fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const 
     long long oseg = -1;
     auto store_out = [&]() {
         cf* yb = y + base_of(oseg) + t;
-        if constexpr (ABL == 1 || ABL == 3) {  // ablation builds: no output traffic
+        if constexpr (ABL == 1 || ABL == 3 || ABL == 4) {  // ablation builds: no output traffic
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 if (ov[k].re == 1234.5678f && k >= h2) yb[256 * k] = ov[k];
@@ -518,6 +524,7 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
     }
     if (p.nomem) {  // profiling ablations (h2 = 1 only): 1 no HBM traffic, 2 no loads, 3 no stores
         if (p.nomem == 2) SDSP_OLS_LAUNCH(true, 2, 1);
+        else if (p.nomem == 4) SDSP_OLS_LAUNCH(true, 4, 1);
         else if (p.nomem == 3) SDSP_OLS_LAUNCH(true, 3, 1);
         else SDSP_OLS_LAUNCH(true, 1, 1);
     } else if (p.interleave && h2 == 1 && p.nt) {

@@ -353,7 +353,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
         case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
         case SDSP_TUNE_OLS_NONTEMPORAL: h->ols_nt = value & 7; break;
         case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 3) ? value : 0; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 4) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }
