@@ -129,7 +129,8 @@ typedef enum {
     SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: 1 (default) = streaming M=1024 kernel where it applies, 0 = per-frame */
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
     SDSP_TUNE_OLS_NONTEMPORAL = 10, /* overlap-save streaming loads (bit 0) / stores (bit 1) */
-    SDSP_TUNE_OLS_WAVE = 11         /* overlap-save: 1 = wave-per-segment N=1024 kernel (L <= 257) */
+    SDSP_TUNE_OLS_WAVE = 11,        /* overlap-save: 1 = wave-per-segment N=1024 kernel (L <= 257) */
+    SDSP_TUNE_OLS_PACKED = 12       /* overlap-save: interior segments in packed-FP32 arithmetic (L <= 1025) */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */

@@ -321,7 +321,7 @@ fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const 
             oseg = seg;
             store_out();
         } else {
-            ols_segment(v, rA, rB, w1, w2, Hr, t, [&] {
+            ols_segment<ABL == 4>(v, rA, rB, w1, w2, Hr, t, [&] {
                 if (oseg >= 0) store_out();
                 load(nxt);
             });
@@ -332,6 +332,41 @@ fir_ols4096_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const 
     }
     if (!(NT & 4) && oseg >= 0) store_out();
     for (; seg < s1; seg += sstep) boundary(seg);
+}
+
+// Boundary segments only (first segments whose window starts before the stream,
+// last ones whose window runs past its end), for calls whose interior segments
+// run in the packed kernel (kern_fir_ols_pk.hip): block b takes segment b when
+// b < lo, else segment hi + (b - lo).
+__global__ void __launch_bounds__(256)
+fir_ols4096_edge_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const cf* __restrict__ Hs,
+                        const cf* __restrict__ tw1, const cf* __restrict__ tw2, cf* __restrict__ y, long long n,
+                        int Lm1, int h2, long long lo, long long hi) {
+    __shared__ __attribute__((aligned(16))) cf lds[2 * kRegion];
+    const int ch = blockIdx.y;
+    x += (long long)ch * n;
+    y += (long long)ch * n;
+    hist += (long long)ch * Lm1;
+    const int t = threadIdx.x;
+    const int lo4 = t & 15;
+    cf w1[16], w2[16], Hr[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        w1[k] = tw1[t * 16 + k];
+        w2[k] = tw2[lo4 * 16 + k];
+        Hr[k] = Hs[t * 16 + k];
+    }
+    const long long b = blockIdx.x;
+    const long long sg = b < lo ? b : hi + (b - lo);
+    const long long base = sg * (4096 - 256 * h2) - 256 * h2;
+    cf v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = ext_ld<true>(x, hist, base + 256 * r + t, n, Lm1);
+    ols_segment(v, lds, lds + kRegion, w1, w2, Hr, t, [] {});
+    const long long ob = base + t;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k >= h2 && ob + 256 * k < n) y[ob + 256 * k] = v[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -521,6 +556,21 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
         }
 #undef SDSP_OLS_WAVE
         return hipGetLastError();
+    }
+    if (p.packed && p.interleave && p.nomem != 2 && p.nomem != 3 && !p.nt && h2 >= 1 && h2 <= 4) {
+        // interior segments in packed arithmetic, the boundary ones here
+        long long lo, hi;
+        ols_interior_range((long long)n, h2, &lo, &hi);
+        const long long nedge = lo + (nseg - hi);
+        if (nedge > 0 && !p.nomem) {
+            hipLaunchKernelGGL(fir_ols4096_edge_kernel, dim3((unsigned)nedge, (unsigned)channels), dim3(256), 0, s,
+                               (const cf*)x, (const cf*)hist, (const cf*)p.d_H, (const cf*)p.d_tw1,
+                               (const cf*)p.d_tw2, (cf*)y, (long long)n, L - 1, h2, lo, hi);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        static const int kAbl[7] = {0, 1, 0, 0, 3, 3, 7};
+        return launch_fir_ols_pk(p, x, y, n, channels, num_cus, s, lo, hi, kAbl[p.nomem]);
     }
     if (p.nomem) {  // profiling ablations (h2 = 1 only): 1 no HBM traffic, 2 no loads, 3 no stores
         if (p.nomem == 2) SDSP_OLS_LAUNCH(true, 2, 1);

@@ -105,6 +105,7 @@ struct sdsp_fir {
     OlsPlan ols{};
     DevBuf d_H, d_tw1, d_tw2, d_H1k, d_tw1k;
     bool ols_wave = false;  // wave-per-segment N = 1024 kernel (SDSP_TUNE_OLS_WAVE)
+    bool ols_packed = false;  // packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED)
 };
 
 namespace {
@@ -208,6 +209,7 @@ int ols_build(sdsp_fir* h) {
     h->ols.d_tw1k = hr1k ? h->d_tw1k.p : nullptr;
     h->ols.halo_rows_1k = hr1k;
     h->ols.wave = h->ols_wave && hr1k > 0;
+    h->ols.packed = h->ols_packed;
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -353,7 +355,8 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
         case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
         case SDSP_TUNE_OLS_NONTEMPORAL: h->ols_nt = value & 7; break;
         case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 4) ? value : 0; break;
+        case SDSP_TUNE_OLS_PACKED: h->ols_packed = value != 0; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 6) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }
@@ -364,6 +367,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     h->ols.nt = h->ols_nt;
     h->ols.occ = h->ols_occ;
     h->ols.wave = h->ols_wave && h->ols.halo_rows_1k > 0;
+    h->ols.packed = h->ols_packed;
     return SDSP_OK;
 }
 

@@ -36,7 +36,8 @@ struct OlsPlan {
     bool wide;        // 16-byte lane-pair global loads/stores
     bool interleave;  // segment order across the persistent grid
     bool depth2;      // two segments of loads in flight (8-byte path)
-    int nomem;        // profiling ablation: 1 no HBM traffic, 2 no loads, 3 no stores (outputs invalid)
+    int nomem;        // profiling ablation (outputs invalid): 1 no HBM traffic, 2 no loads, 3 no stores,
+                      // 4 no HBM + no barriers; packed kernel: 5 no HBM + no barriers, 6 also no LDS
     int occ;          // retired (0)
     int nt = 0;       // nontemporal: bit 0 loads, bit 1 stores
     // wave-per-segment N = 1024 kernel (L - 1 <= 256)
@@ -44,10 +45,15 @@ struct OlsPlan {
     void* d_tw1k = nullptr;  // [1024] c32: W1024^m
     int halo_rows_1k = 0;    // HR: 64 HR >= L - 1
     bool wave = false;
+    bool packed = false;  // interior segments in packed-FP32 arithmetic (kern_fir_ols_pk.hip)
 };
 constexpr int kOlsN = 4096;
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
                           size_t channels, int num_cus, hipStream_t s);
+// interior segments [lo, hi) of a call: whole input window and all outputs inside the stream
+void ols_interior_range(long long n, int h2, long long* lo, long long* hi);
+hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, int num_cus,
+                             hipStream_t s, long long lo, long long hi, int ablate);
 
 // polyphase filterbank / interpolator: out[j*M + p] = sum_{i<K} cb[p*K + i] * ext(j - i)
 struct PfbArgs {

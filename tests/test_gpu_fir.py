@@ -149,6 +149,30 @@ def test_fir_fft_wave_kernel_tolerance(dt, cdt, L):
     assert np.abs(y - ref).max() <= bound
 
 
+@pytest.mark.parametrize("L", [2, 64, 256, 257, 513, 1000, 1025])
+@pytest.mark.parametrize("ch", [1, 3])
+def test_fir_fft_packed_kernel_bit_identical(L, ch):
+    # packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED = 12) + boundary-segment kernel vs the
+    # scalar overlap-save kernel: the same IEEE operations per component, so identical bits;
+    # ragged calls cover all-boundary calls (n < one window), history and both edges
+    h = _f32_taps(L, 0.1)
+    h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
+    x = O.synth(20250227, 4, 0, 300000 * ch, complex_=True).reshape(ch, -1) if ch > 1 else \
+        O.synth(20250227, 4, 0, 300000, complex_=True)
+    a = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
+    b = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
+    assert sd.lib().sdsp_fir_set_tuning(a._h, 12, 1) == 0
+    assert sd.lib().sdsp_fir_set_tuning(b._h, 12, 0) == 0
+    cuts = [0, 1, 3000, 7001, 70001, 207713, 300000]
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        xa = x[..., lo:hi]
+        assert bits_equal(a.execute_block(xa), b.execute_block(xa)), (L, ch, lo, hi)
+    ref = O.fir(O.CC64, h.astype(C128), 0.2 + 0j).execute_block((x[-1] if ch > 1 else x).astype(C128))
+    a.reset()
+    y = a.execute_block(x)
+    assert rel_rms(y[-1] if ch > 1 else y, ref) <= 1e-6
+
+
 def test_fir_fft_matches_exact_kernel_across_calls():
     h = _f32_taps(256, 0.1)
     x = O.synth(7, 3, 0, 200000, complex_=True)
