@@ -115,10 +115,11 @@ SDSP_API int sdsp_fir_set_algo(sdsp_fir* h, int algo);
 SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
 /* kernel-variant knobs (performance only; results are identical across values, except
  * SDSP_TUNE_OLS_ABLATE_NOMEM, a profiling ablation that skips HBM traffic and leaves the
- * output unwritten).  WIDE / DEPTH2 / OCCUPANCY name overlap-save variants that were
- * measured slower and retired: only 0 is accepted (SDSP_E_UNSUPPORTED otherwise). */
+ * output unwritten).  Overlap-save defaults: PACKED = 1, WIDE = 1 (16-byte accesses in the
+ * packed kernel), SEGS_PER_BLOCK = 16.  DEPTH2 / OCCUPANCY name variants that were measured
+ * slower and retired: only 0 is accepted (SDSP_E_UNSUPPORTED otherwise). */
 typedef enum {
-    SDSP_TUNE_OLS_WIDE = 1,
+    SDSP_TUNE_OLS_WIDE = 1,        /* packed overlap-save: 1 (default) = 16-byte global accesses */
     SDSP_TUNE_OLS_INTERLEAVE = 2,  /* 1 (default): segments interleaved across the persistent grid */
     SDSP_TUNE_OLS_DEPTH2 = 3,
     SDSP_TUNE_OLS_ABLATE_NOMEM = 4,
@@ -130,7 +131,8 @@ typedef enum {
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
     SDSP_TUNE_OLS_NONTEMPORAL = 10, /* overlap-save streaming loads (bit 0) / stores (bit 1) */
     SDSP_TUNE_OLS_WAVE = 11,        /* overlap-save: 1 = wave-per-segment N=1024 kernel (L <= 257) */
-    SDSP_TUNE_OLS_PACKED = 12       /* overlap-save: interior segments in packed-FP32 arithmetic (L <= 1025) */
+    SDSP_TUNE_OLS_PACKED = 12,      /* overlap-save: interior segments in packed-FP32 arithmetic (L <= 1025) */
+    SDSP_TUNE_OLS_SEGS_PER_BLOCK = 13 /* packed overlap-save: 0 = persistent grid, k = k consecutive segments per workgroup */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */

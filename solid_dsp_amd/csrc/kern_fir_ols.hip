@@ -518,6 +518,20 @@ fir_ols1024_wave_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, c
     for (; seg < nseg; seg += GW) boundary(seg);
 }
 
+// interior segment range of a call: [lo, hi) with input window and outputs in range
+void ols_interior_range(long long n, int h2, long long* lo, long long* hi) {
+    const long long V = 4096 - 256LL * h2, H = 256LL * h2;
+    const long long nseg = (n + V - 1) / V;
+    long long a = (H + V - 1) / V;  // first s with s V - H >= 0
+    if (a > nseg) a = nseg;
+    // last s with s V - H + 4096 <= n
+    long long b = n - 4096 + H >= 0 ? (n - 4096 + H) / V + 1 : 0;
+    if (b > nseg) b = nseg;
+    if (b < a) b = a;
+    *lo = a;
+    *hi = b;
+}
+
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
                           size_t channels, int num_cus, hipStream_t s) {
     if (n == 0) return hipSuccess;
@@ -557,7 +571,10 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
 #undef SDSP_OLS_WAVE
         return hipGetLastError();
     }
-    if (p.packed && p.interleave && p.nomem != 2 && p.nomem != 3 && !p.nt && h2 >= 1 && h2 <= 4) {
+    // packed interior kernel: by default only with 16-byte rows (its 8-byte form is slower than this file's)
+    const bool rows16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0 &&
+                        (channels == 1 || n % 2 == 0);
+    if (p.packed && (rows16 || !p.wide) && p.interleave && p.nomem != 2 && p.nomem != 3 && h2 >= 1 && h2 <= 4) {
         // interior segments in packed arithmetic, the boundary ones here
         long long lo, hi;
         ols_interior_range((long long)n, h2, &lo, &hi);
@@ -569,8 +586,11 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
-        static const int kAbl[7] = {0, 1, 0, 0, 3, 3, 7};
-        return launch_fir_ols_pk(p, x, y, n, channels, num_cus, s, lo, hi, kAbl[p.nomem]);
+        static const int kAbl[8] = {0, 1, 0, 0, 3, 3, 7, 8};
+        const int abl = kAbl[p.nomem];
+        if (p.packed <= 2) return pk_default::launch_fir_ols_pk(p, x, y, n, channels, num_cus, s, lo, hi, abl);
+        if (p.packed <= 4) return pk_ilp::launch_fir_ols_pk(p, x, y, n, channels, num_cus, s, lo, hi, abl);
+        return pk_iilp::launch_fir_ols_pk(p, x, y, n, channels, num_cus, s, lo, hi, abl);
     }
     if (p.nomem) {  // profiling ablations (h2 = 1 only): 1 no HBM traffic, 2 no loads, 3 no stores
         if (p.nomem == 2) SDSP_OLS_LAUNCH(true, 2, 1);

@@ -19,56 +19,67 @@
 //     callers index through kout() instead of copying into natural order;
 //   * the twiddle and spectrum registers are made opaque once per segment so
 //     swizzled copies of them are not hoisted out of the loop.
+//
+// The file is compiled once per scheduling strategy (Makefile: SDSP_PK_NS names
+// the namespace, e.g. -mllvm -amdgpu-sched-strategy=max-ilp for pk_ilp), so the
+// strategies can be A/B'd in one process through SDSP_TUNE_OLS_PACKED.
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 
+#ifndef SDSP_PK_NS
+#define SDSP_PK_NS pk_default
+#endif
+
 namespace sdsp {
+namespace SDSP_PK_NS {
 
 namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
 
-// Complex helpers as single VOP3P instructions: op_sel / op_sel_hi pick the
-// half of each 64-bit source that feeds the low / high result, neg_lo / neg_hi
-// negate a source for that result.  Written as asm because the backend turns
-// a swapped, half-negated operand ({b.y, -b.x}) into v_xor + v_mov pairs.
-// Per component each helper performs the operation sequence of its scalar
-// counterpart in kern_fir_ols.hip (cmul, cmulc, dft4, tw16), so results are
-// bit-identical.
+// Complex helpers.  Per component each performs the operation sequence of its
+// scalar counterpart in kern_fir_ols.hip (cmul, cmulc, dft4, tw16), so results
+// are bit-identical.  A swapped, half-negated operand ({b.y, -b.x}) is written
+// as a product or fma with a +-1 pair (exact; the pair lives in an SGPR pair and
+// the swap becomes op_sel): the backend does not fold a one-lane negation into
+// neg_lo / neg_hi and would emit v_xor + v_mov pairs instead.
+//
+// The table products a * w (two per complex multiply) exist in two builds:
+// ASM = true issues them as two VOP3P instructions with op_sel / neg modifiers
+// (inline asm: the scheduler sees no latency for them); ASM = false uses three
+// compiler-visible instructions.
+constexpr f2 kPM = {1.0f, -1.0f};
+constexpr f2 kMP = {-1.0f, 1.0f};
 
 // a * b = {fma(a.x, b.x, -(a.y b.y)), fma(a.x, b.y, a.y b.x)}
-__device__ __forceinline__ f2 pmul(f2 a, f2 b) {
-    f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(t) : "v"(a), "v"(b));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
-    return r;
+template <bool ASM> __device__ __forceinline__ f2 pmul(f2 a, f2 b) {
+    if constexpr (ASM) {
+        f2 t, r;
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+        return r;
+    } else {
+        return __builtin_elementwise_fma(a.xx, b, (a.yy * b.yx) * kMP);
+    }
 }
 // a * conj(b) = {fma(a.x, b.x, a.y b.y), fma(a.y, b.x, -(a.x b.y))}
-__device__ __forceinline__ f2 pmulc(f2 a, f2 b) {
-    f2 t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
-    return r;
+template <bool ASM> __device__ __forceinline__ f2 pmulc(f2 a, f2 b) {
+    if constexpr (ASM) {
+        f2 t, r;
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+        return r;
+    } else {
+        return __builtin_elementwise_fma(a, b.xx, (a.yx * b.yy) * kPM);
+    }
 }
 // b + (-j) e = {b.x + e.y, b.y - e.x}
-__device__ __forceinline__ f2 padd_mj(f2 b, f2 e) {
-    f2 r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(b), "v"(e));
-    return r;
-}
+__device__ __forceinline__ f2 padd_mj(f2 b, f2 e) { return __builtin_elementwise_fma(e.yx, kPM, b); }
 // b + (+j) e = {b.x - e.y, b.y + e.x}
-__device__ __forceinline__ f2 padd_pj(f2 b, f2 e) {
-    f2 r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(b), "v"(e));
-    return r;
-}
-// (-j) v = {v.y, -v.x} (forward) / (+j) v = {-v.y, v.x} (inverse), exact
-template <bool INV> __device__ __forceinline__ f2 prot(f2 v) {
-    f2 r;
-    if constexpr (INV) asm("v_pk_mul_f32 %0, %1, 1.0 op_sel:[1,0] op_sel_hi:[0,0] neg_lo:[0,1]" : "=v"(r) : "v"(v));
-    else asm("v_pk_mul_f32 %0, %1, 1.0 op_sel:[1,0] op_sel_hi:[0,0] neg_hi:[0,1]" : "=v"(r) : "v"(v));
-    return r;
-}
+__device__ __forceinline__ f2 padd_pj(f2 b, f2 e) { return __builtin_elementwise_fma(e.yx, kMP, b); }
+// (-j) v = {v.y, -v.x} (forward) / (+j) v = {-v.y, v.x} (inverse)
+template <bool INV> __device__ __forceinline__ f2 prot(f2 v) { return v.yx * (INV ? kMP : kPM); }
 template <bool INV> __device__ __forceinline__ void pdft4(f2& x0, f2& x1, f2& x2, f2& x3) {
     const f2 a = x0 + x2, b = x0 - x2, c = x1 + x3, e = x1 - x3;
     x0 = a + c;
@@ -86,22 +97,18 @@ constexpr float kC1 = 0.92387953251128674f;  // cos(pi/8)
 constexpr float kS1 = 0.38268343236508978f;  // sin(pi/8)
 constexpr float kR2 = 0.70710678118654752f;  // sqrt(1/2)
 
-// v * (cr + j ci) for compile-time cr, ci (the constant pair is a splat-free operand)
+// v * (cr + j ci) for compile-time cr, ci
 __device__ __forceinline__ f2 pmulk(f2 v, float cr, float ci) {
     return __builtin_elementwise_fma(v.xx, f2{cr, ci}, v.yy * f2{-ci, cr});
 }
-// kR2 * (v.x + s v.y, v.y - s v.x)  (tw16 m = 2)
+// tw16 m = 2: kR2 * (v.x + s v.y, v.y - s v.x)
 template <bool INV> __device__ __forceinline__ f2 ptw2(f2 v) {
     return (INV ? padd_pj(v, v) : padd_mj(v, v)) * kR2;
 }
-// kR2 * (-v.x + s v.y, -v.y - s v.x)  (tw16 m = 6): forward {v.y - v.x, -v.y - v.x}
+// tw16 m = 6: kR2 * (-v.x + s v.y, -v.y - s v.x)
 template <bool INV> __device__ __forceinline__ f2 ptw6(f2 v) {
-    f2 r;
-    if constexpr (INV)  // {-v.x - v.y, v.x - v.y}
-        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1] neg_lo:[1,1] neg_hi:[0,1]" : "=v"(r) : "v"(v), "v"(v));
-    else  // {v.y - v.x, -v.y - v.x}
-        asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[1,1]" : "=v"(r) : "v"(v), "v"(v));
-    return r * kR2;
+    if constexpr (INV) return __builtin_elementwise_fma(v.xx, kMP, -v.yy) * kR2;  // {-v.x - v.y, v.x - v.y}
+    else return __builtin_elementwise_fma(v.yy, kPM, -v.xx) * kR2;                 // {v.y - v.x, -v.y - v.x}
 }
 template <bool INV, int m> __device__ __forceinline__ f2 ptw16(f2 v) {
     constexpr float s = INV ? -1.0f : 1.0f;
@@ -113,6 +120,13 @@ template <bool INV, int m> __device__ __forceinline__ f2 ptw16(f2 v) {
     else if constexpr (m == 6) return ptw6<INV>(v);
     else if constexpr (m == 9) return pmulk(v, -kC1, s * kS1);
     else return v;
+}
+
+// lanes 16..31 of a <-> lanes 0..15 of b, in each half wave (v_permlane16_swap_b32)
+__device__ __forceinline__ void swap16(float& a, float& b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
 }
 
 // X[k] of a DFT16 lives at v[kout(k)] (stage order, no reordering copy)
@@ -144,12 +158,23 @@ __device__ __forceinline__ int bidx(int r, int c) { return r * 16 + ((((c >> 1) 
 
 // ABL: profiling ablations (outputs invalid), same arithmetic.  Bit 0: no HBM loads
 // or stores; bit 1: no workgroup barriers; bit 2: no LDS (transposes become
-// register renames)
-template <int H2, int ABL>
+// register renames).  ABL = 8: HBM traffic only (no arithmetic, LDS or barriers)
+//
+// W16: 16-byte global accesses.  Lane t then owns column
+//     col(t) = 32 (t >> 5) + 2 (t & 15) + ((t >> 4) & 1)
+// instead of t: a lane loads two adjacent columns (X, X + 1), X = col - (t>>4 & 1),
+// of one row (rows 2i and 2i + 1 for the lower / upper 16 lanes of each 32), and
+// one v_permlane16_swap per dword (lanes 16..31 of the first operand <-> lanes
+// 0..15 of the second) turns the pair into column X (lower lane) and X + 1 (upper
+// lane) over rows 2i, 2i + 1.  The same swap turns P5's columns back into row
+// pairs for dwordx4 stores.  P1 writes and P5 reads LDS column col(t) (a
+// permutation of the columns inside each wave, still conflict-free) and w1 is the
+// table row of col(t); P2..P4 are unchanged.
+template <int H2, int ABL, bool ASM, bool W16, int NT = 0>
 __global__ void __launch_bounds__(256, 2)
 fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const f2* __restrict__ tw1,
                       const f2* __restrict__ tw2, f2* __restrict__ y, long long n, long long seg_lo,
-                      long long seg_hi) {
+                      long long seg_hi, long long per) {
     __shared__ __attribute__((aligned(16))) f2 lds[2 * kRegion];
     f2* const rA = lds;
     f2* const rB = lds + kRegion;
@@ -158,22 +183,47 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
     y += (long long)ch * n;
     const int t = threadIdx.x;
     const int hi4 = t >> 4, lo4 = t & 15;
+    const int up = (t >> 4) & 1;                   // W16: upper 16 lanes of a 32
+    const int colX = 32 * (t >> 5) + 2 * (t & 15);  // W16: first column of the lane pair
+    const int col = W16 ? colX + up : t;
     f2 w1[16], w2[16], Hr[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        w1[k] = tw1[t * 16 + k];
+        w1[k] = tw1[col * 16 + k];
         w2[k] = tw2[lo4 * 16 + k];
         Hr[k] = Hs[t * 16 + k];
     }
     constexpr int V = 4096 - 256 * H2;
-    // interior segments [seg_lo, seg_hi), interleaved over the persistent grid
-    const long long sstep = gridDim.x;
-    long long seg = seg_lo + blockIdx.x;
-    f2 nv[16];
+    // interior segments [seg_lo, seg_hi): per == 0, interleaved over a persistent
+    // grid; per > 0, `per` consecutive segments per workgroup (the dispatcher then
+    // keeps the resident workgroups on one compact window of the stream)
+    long long sstep, seg;
+    if (per == 0) {
+        sstep = gridDim.x;
+        seg = seg_lo + blockIdx.x;
+    } else {
+        sstep = 1;
+        seg = seg_lo + (long long)blockIdx.x * per;
+        const long long e = seg + per;
+        if (e < seg_hi) seg_hi = e;
+    }
+    f2 nv[16];      // 8-byte path: lane's column over rows
+    float4 nq[8];   // W16 path: row 2i + up, columns colX, colX + 1
     auto load = [&](long long sg) {
         if constexpr (ABL & 1) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) nv[r] = f2{(float)(t + r), (float)(sg & 1023)};
+        } else if constexpr (W16) {
+            const float4* xb = reinterpret_cast<const float4*>(x + sg * V - 256 * H2 + 256 * up + colX);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if constexpr (NT & 1) {
+                    const f4v q = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(xb + 256 * i));
+                    nq[i] = make_float4(q.x, q.y, q.z, q.w);
+                } else {
+                    nq[i] = xb[256 * i];
+                }
+            }
         } else {
             const f2* xb = x + sg * V - 256 * H2 + t;
 #pragma unroll
@@ -186,13 +236,28 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
     f2 ov[16];
     long long oseg = -1;
     auto store_out = [&] {
-        f2* yb = y + oseg * V - 256 * H2 + t;
+        if constexpr (W16 && !(ABL & 1)) {
+            float4* yb = reinterpret_cast<float4*>(y + oseg * V - 256 * H2 + 256 * up + colX);
 #pragma unroll
-        for (int k = H2; k < 16; ++k) {
-            if constexpr (ABL & 1) {
-                if (ov[k].x == 1234.5678f) yb[256 * k] = ov[k];
-            } else {
-                yb[256 * k] = ov[k];
+            for (int i = 0; i < 8; ++i) {
+                if (2 * i + 1 < H2) continue;  // both rows are halo
+                float4 q = make_float4(ov[2 * i].x, ov[2 * i].y, ov[2 * i + 1].x, ov[2 * i + 1].y);
+                swap16(q.x, q.z);
+                swap16(q.y, q.w);
+                if (2 * i >= H2 || up) {  // row 2i is halo when 2i < H2: only the upper lanes (row 2i + 1) store
+                    if constexpr (NT & 2) __builtin_nontemporal_store(f4v{q.x, q.y, q.z, q.w}, reinterpret_cast<f4v*>(yb + 256 * i));
+                    else yb[256 * i] = q;
+                }
+            }
+        } else {
+            f2* yb = y + oseg * V - 256 * H2 + t;
+#pragma unroll
+            for (int k = H2; k < 16; ++k) {
+                if constexpr (ABL & 1) {
+                    if (ov[k].x == 1234.5678f) yb[256 * k] = ov[k];
+                } else {
+                    yb[256 * k] = ov[k];
+                }
             }
         }
     };
@@ -218,13 +283,34 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
 #pragma unroll
         for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(w1[k]), "+v"(w2[k]), "+v"(Hr[k]));
         f2 v[16];
+        if constexpr (W16 && !(ABL & 1)) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = nv[r];
+            for (int i = 0; i < 8; ++i) {
+                float4 q = nq[i];
+                swap16(q.x, q.z);
+                swap16(q.y, q.w);
+                v[2 * i] = f2{q.x, q.y};
+                v[2 * i + 1] = f2{q.z, q.w};
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = nv[r];
+        }
         const long long nxt = seg + sstep < seg_hi ? seg + sstep : seg;
+        if constexpr (ABL == 8) {  // the kernel's HBM traffic alone: same grid, loads and deferred stores
+#pragma unroll
+            for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[k]));
+            if (oseg >= 0) store_out();
+            load(nxt);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) ov[k] = v[k];
+            oseg = seg;
+            continue;
+        }
         // P1: DFT over n2 -> k0, twiddle, A[k0][t]
         pdft16<false>(v);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) sto(rA, k * kRowA + t, k, pmul(v[kout(k)], w1[k]));
+        for (int k = 0; k < 16; ++k) sto(rA, k * kRowA + col, k, pmul<ASM>(v[kout(k)], w1[k]));
         if (oseg >= 0) store_out();
         load(nxt);
         bar();
@@ -233,7 +319,7 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         for (int k = 0; k < 16; ++k) v[k] = ldo(rA, hi4 * kRowA + 16 * k + lo4, k);
         pdft16<false>(v);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) sto(rB, bidx(16 * hi4 + k, lo4), k, pmul(v[kout(k)], w2[k]));
+        for (int k = 0; k < 16; ++k) sto(rB, bidx(16 * hi4 + k, lo4), k, pmul<ASM>(v[kout(k)], w2[k]));
         bar();
         // P3: lane (k0=hi4, k1=lo4) reads its row over n0
         {
@@ -253,14 +339,14 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         pdft16<false>(v);
         f2 u[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) u[k] = pmul(v[kout(k)], Hr[k]);
+        for (int k = 0; k < 16; ++k) u[k] = pmul<ASM>(v[kout(k)], Hr[k]);
         pdft16<true>(u);
         {
             float4* row = reinterpret_cast<float4*>(rA + t * 16);
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
-                const f2 a = pmulc(u[kout(2 * p)], w2[2 * p]);
-                const f2 b = pmulc(u[kout(2 * p + 1)], w2[2 * p + 1]);
+                const f2 a = pmulc<ASM>(u[kout(2 * p)], w2[2 * p]);
+                const f2 b = pmulc<ASM>(u[kout(2 * p + 1)], w2[2 * p + 1]);
                 if constexpr (ABL & 4) {
                     tmp[2 * p] = a;
                     tmp[2 * p + 1] = b;
@@ -279,7 +365,7 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         bar();
         // P5: lane t=(n1,n0) reads k0
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = pmulc(ldo(rB, k * kRowA + t, k), w1[k]);
+        for (int k = 0; k < 16; ++k) v[k] = pmulc<ASM>(ldo(rB, k * kRowA + col, k), w1[k]);
         pdft16<true>(v);
 #pragma unroll
         for (int k = 0; k < 16; ++k) ov[k] = v[kout(k)];
@@ -290,35 +376,48 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
     if (oseg >= 0) store_out();
 }
 
-// interior segment range of a call: [lo, hi) with input window and outputs in range
-void ols_interior_range(long long n, int h2, long long* lo, long long* hi) {
-    const long long V = 4096 - 256LL * h2, H = 256LL * h2;
-    const long long nseg = (n + V - 1) / V;
-    long long a = (H + V - 1) / V;  // first s with s V - H >= 0
-    if (a > nseg) a = nseg;
-    // last s with s V - H + 4096 <= n
-    long long b = n - 4096 + H >= 0 ? (n - 4096 + H) / V + 1 : 0;
-    if (b > nseg) b = nseg;
-    if (b < a) b = a;
-    *lo = a;
-    *hi = b;
-}
-
 hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, int num_cus,
                              hipStream_t s, long long lo, long long hi, int ablate) {
     if (hi <= lo) return hipSuccess;
+    const long long per = p.segs_per_block;
+    // 16-byte accesses need 16-byte aligned rows in every channel
+    const bool w16 = p.wide && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0 &&
+                     (channels == 1 || n % 2 == 0);
     long long blocks = (long long)num_cus * 2;
-    if (blocks > hi - lo) blocks = hi - lo;
+    if (per > 0) blocks = (hi - lo + per - 1) / per;
+    else if (blocks > hi - lo) blocks = hi - lo;
     dim3 grid((unsigned)blocks, (unsigned)channels);
+#define SDSP_OLS_PK_W(HV, A, M, W)                                                                               \
+    hipLaunchKernelGGL((fir_ols4096_pk_kernel<HV, A, M, W>), grid, dim3(256), 0, s, (const f2*)x, (const f2*)p.d_H, \
+                       (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per)
 #define SDSP_OLS_PK_L(HV, A)                                                                                     \
-    hipLaunchKernelGGL((fir_ols4096_pk_kernel<HV, A>), grid, dim3(256), 0, s, (const f2*)x, (const f2*)p.d_H,     \
-                       (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi)
+    do {                                                                                                         \
+        if (p.packed % 2 == 0) {                                                                                 \
+            if (w16) SDSP_OLS_PK_W(HV, A, false, true); else SDSP_OLS_PK_W(HV, A, false, false);                 \
+        } else {                                                                                                 \
+            if (w16) SDSP_OLS_PK_W(HV, A, true, true); else SDSP_OLS_PK_W(HV, A, true, false);                   \
+        }                                                                                                        \
+    } while (0)
 #define SDSP_OLS_PK(HV) SDSP_OLS_PK_L(HV, 0)
+    if (w16 && p.nt && p.halo_rows == 1 && !ablate) {  // nontemporal hints (bit 0 loads, bit 1 stores), h2 = 1
+#define SDSP_OLS_PK_NT(M, NTV)                                                                                   \
+    hipLaunchKernelGGL((fir_ols4096_pk_kernel<1, 0, M, true, NTV>), grid, dim3(256), 0, s, (const f2*)x,         \
+                       (const f2*)p.d_H, (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per)
+        const int ntv = p.nt & 3;
+        if (p.packed % 2 == 0) {
+            if (ntv == 1) SDSP_OLS_PK_NT(false, 1); else if (ntv == 2) SDSP_OLS_PK_NT(false, 2); else SDSP_OLS_PK_NT(false, 3);
+        } else {
+            if (ntv == 1) SDSP_OLS_PK_NT(true, 1); else if (ntv == 2) SDSP_OLS_PK_NT(true, 2); else SDSP_OLS_PK_NT(true, 3);
+        }
+#undef SDSP_OLS_PK_NT
+        return hipGetLastError();
+    }
     if (ablate) {  // profiling ablations, h2 = 1 only
         if (p.halo_rows != 1) return hipErrorInvalidValue;
         if (ablate == 1) SDSP_OLS_PK_L(1, 1);
         else if (ablate == 3) SDSP_OLS_PK_L(1, 3);
         else if (ablate == 7) SDSP_OLS_PK_L(1, 7);
+        else if (ablate == 8) SDSP_OLS_PK_L(1, 8);
         else return hipErrorInvalidValue;
         return hipGetLastError();
     }
@@ -331,7 +430,9 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
     }
 #undef SDSP_OLS_PK
 #undef SDSP_OLS_PK_L
+#undef SDSP_OLS_PK_W
     return hipGetLastError();
 }
 
+}  // namespace SDSP_PK_NS
 }  // namespace sdsp

@@ -97,7 +97,7 @@ struct sdsp_fir {
     DevBuf stage_in, stage_out;
     // overlap-save plan
     bool ols_ok = false;
-    bool ols_wide = false, ols_interleave = true, ols_depth2 = false;
+    bool ols_wide = true, ols_interleave = true, ols_depth2 = false;
     int ols_nomem = 0;
     int ols_nt = 0;
     int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
@@ -105,7 +105,8 @@ struct sdsp_fir {
     OlsPlan ols{};
     DevBuf d_H, d_tw1, d_tw2, d_H1k, d_tw1k;
     bool ols_wave = false;  // wave-per-segment N = 1024 kernel (SDSP_TUNE_OLS_WAVE)
-    bool ols_packed = false;  // packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED)
+    int ols_segs = 16;  // SDSP_TUNE_OLS_SEGS_PER_BLOCK
+    int ols_packed = 1;  // packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED): 0 off, 1..6 builds
 };
 
 namespace {
@@ -210,6 +211,7 @@ int ols_build(sdsp_fir* h) {
     h->ols.halo_rows_1k = hr1k;
     h->ols.wave = h->ols_wave && hr1k > 0;
     h->ols.packed = h->ols_packed;
+    h->ols.segs_per_block = h->ols_segs;
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -347,7 +349,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     switch (key) {
         // retired overlap-save variants (measured slower): only their default is accepted
-        case SDSP_TUNE_OLS_WIDE:
+        case SDSP_TUNE_OLS_WIDE: h->ols_wide = value != 0; break;  // packed kernel only
         case SDSP_TUNE_OLS_DEPTH2:
         case SDSP_TUNE_OLS_OCCUPANCY:
             if (value != 0) return SDSP_E_UNSUPPORTED;
@@ -355,8 +357,9 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
         case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
         case SDSP_TUNE_OLS_NONTEMPORAL: h->ols_nt = value & 7; break;
         case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
-        case SDSP_TUNE_OLS_PACKED: h->ols_packed = value != 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 6) ? value : 0; break;
+        case SDSP_TUNE_OLS_SEGS_PER_BLOCK: h->ols_segs = value > 0 ? value : 0; break;
+        case SDSP_TUNE_OLS_PACKED: h->ols_packed = (value >= 0 && value <= 6) ? value : 0; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 7) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }
@@ -368,6 +371,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     h->ols.occ = h->ols_occ;
     h->ols.wave = h->ols_wave && h->ols.halo_rows_1k > 0;
     h->ols.packed = h->ols_packed;
+    h->ols.segs_per_block = h->ols_segs;
     return SDSP_OK;
 }
 

@@ -37,7 +37,8 @@ struct OlsPlan {
     bool interleave;  // segment order across the persistent grid
     bool depth2;      // two segments of loads in flight (8-byte path)
     int nomem;        // profiling ablation (outputs invalid): 1 no HBM traffic, 2 no loads, 3 no stores,
-                      // 4 no HBM + no barriers; packed kernel: 5 no HBM + no barriers, 6 also no LDS
+                      // 4 no HBM + no barriers; packed kernel: 5 no HBM + no barriers, 6 also no LDS,
+                      // 7 HBM traffic only
     int occ;          // retired (0)
     int nt = 0;       // nontemporal: bit 0 loads, bit 1 stores
     // wave-per-segment N = 1024 kernel (L - 1 <= 256)
@@ -45,15 +46,25 @@ struct OlsPlan {
     void* d_tw1k = nullptr;  // [1024] c32: W1024^m
     int halo_rows_1k = 0;    // HR: 64 HR >= L - 1
     bool wave = false;
-    bool packed = false;  // interior segments in packed-FP32 arithmetic (kern_fir_ols_pk.hip)
+    int packed = 0;  // packed-FP32 interior kernel (kern_fir_ols_pk.hip): odd = asm table products, even = compiler-
+                     // visible; 1-2 default scheduler, 3-4 max-ilp, 5-6 iterative-ilp
+    int segs_per_block = 0;  // packed kernel: 0 persistent interleaved grid, > 0 consecutive segments per workgroup
 };
 constexpr int kOlsN = 4096;
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
                           size_t channels, int num_cus, hipStream_t s);
 // interior segments [lo, hi) of a call: whole input window and all outputs inside the stream
 void ols_interior_range(long long n, int h2, long long* lo, long long* hi);
-hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, int num_cus,
-                             hipStream_t s, long long lo, long long hi, int ablate);
+// packed interior kernel, one build per scheduling strategy (kern_fir_ols_pk.hip)
+#define SDSP_DECL_OLS_PK(NS)                                                                                      \
+    namespace NS {                                                                                                \
+    hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, int num_cus, \
+                                 hipStream_t s, long long lo, long long hi, int ablate);                          \
+    }
+SDSP_DECL_OLS_PK(pk_default)
+SDSP_DECL_OLS_PK(pk_ilp)
+SDSP_DECL_OLS_PK(pk_iilp)
+#undef SDSP_DECL_OLS_PK
 
 // polyphase filterbank / interpolator: out[j*M + p] = sum_{i<K} cb[p*K + i] * ext(j - i)
 struct PfbArgs {

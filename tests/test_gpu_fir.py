@@ -149,24 +149,31 @@ def test_fir_fft_wave_kernel_tolerance(dt, cdt, L):
     assert np.abs(y - ref).max() <= bound
 
 
-@pytest.mark.parametrize("L", [2, 64, 256, 257, 513, 1000, 1025])
+@pytest.mark.parametrize("L,pk,per,wide", [(L, 1, 0, 0) for L in (2, 64, 256, 513, 1000)] +
+                         [(L, pk, 0, 0) for L in (257, 1025) for pk in range(1, 7)] +
+                         [(257, 5, per, 0) for per in (1, 3, 16)] +
+                         [(L, pk, 0, 1) for L in (64, 513, 700, 1025) for pk in (5, 6)] +
+                         [(257, 5, 16, 1), (700, 1, 3, 1)])
 @pytest.mark.parametrize("ch", [1, 3])
-def test_fir_fft_packed_kernel_bit_identical(L, ch):
-    # packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED = 12) + boundary-segment kernel vs the
-    # scalar overlap-save kernel: the same IEEE operations per component, so identical bits;
-    # ragged calls cover all-boundary calls (n < one window), history and both edges
+def test_fir_fft_packed_kernel_bit_identical(L, pk, per, wide, ch):
+    # packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED = 12, builds 1..6: table products as asm
+    # or compiler-visible, three scheduling strategies) + boundary-segment kernel vs the scalar
+    # overlap-save kernel: the same IEEE operations per component, so identical bits; ragged
+    # calls cover all-boundary calls (n < one window), history and both edges
     h = _f32_taps(L, 0.1)
     h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
     x = O.synth(20250227, 4, 0, 300000 * ch, complex_=True).reshape(ch, -1) if ch > 1 else \
         O.synth(20250227, 4, 0, 300000, complex_=True)
     a = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
     b = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
-    assert sd.lib().sdsp_fir_set_tuning(a._h, 12, 1) == 0
+    assert sd.lib().sdsp_fir_set_tuning(a._h, 12, pk) == 0
+    assert sd.lib().sdsp_fir_set_tuning(a._h, 13, per) == 0
+    assert sd.lib().sdsp_fir_set_tuning(a._h, 1, wide) == 0  # 16-byte accesses (even n or one channel)
     assert sd.lib().sdsp_fir_set_tuning(b._h, 12, 0) == 0
-    cuts = [0, 1, 3000, 7001, 70001, 207713, 300000]
+    cuts = [0, 1, 3000, 7001, 70001, 207714, 300000]
     for lo, hi in zip(cuts[:-1], cuts[1:]):
         xa = x[..., lo:hi]
-        assert bits_equal(a.execute_block(xa), b.execute_block(xa)), (L, ch, lo, hi)
+        assert bits_equal(a.execute_block(xa), b.execute_block(xa)), (L, pk, per, wide, ch, lo, hi)
     ref = O.fir(O.CC64, h.astype(C128), 0.2 + 0j).execute_block((x[-1] if ch > 1 else x).astype(C128))
     a.reset()
     y = a.execute_block(x)

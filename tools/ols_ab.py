@@ -27,6 +27,7 @@ def main(rounds=8, log2n=30):
         nt = cfg[5] if len(cfg) > 5 else 0
         wave = cfg[6] if len(cfg) > 6 else 0
         pk = cfg[7] if len(cfg) > 7 else 0
+        per = cfg[8] if len(cfg) > 8 else 0
         f = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, algo=sd.ALGO_FFT)
         sd.lib().sdsp_fir_set_tuning(f._h, 1, wide)
         sd.lib().sdsp_fir_set_tuning(f._h, 2, inter)
@@ -36,7 +37,8 @@ def main(rounds=8, log2n=30):
         sd.lib().sdsp_fir_set_tuning(f._h, 10, nt)
         sd.lib().sdsp_fir_set_tuning(f._h, 11, wave)
         sd.lib().sdsp_fir_set_tuning(f._h, 12, pk)
-        variants[f"wave{wave}_pk{pk}_inter{inter}_nt{nt}_nomem{nomem}"] = f
+        sd.lib().sdsp_fir_set_tuning(f._h, 13, per)
+        variants[f"wave{wave}_pk{pk}_per{per}_w{wide}_inter{inter}_nt{nt}_nomem{nomem}"] = f
     s = torch.cuda.current_stream()
     times = {k: [] for k in variants}
     for k, f in variants.items():
