@@ -48,15 +48,17 @@ def parse():
     return p.parse_args()
 
 
-def load_traffic(config, log2n, algo):
+def load_traffic(config, log2n, algo, kernel=""):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (profiles/*/pmc_summary_cfg*.json written by tools/pmc_summary.py), or None."""
+    (profiles/*/pmc_summary_cfg*.json written by tools/pmc_summary.py), or None.
+    The summary must name the kernel this run launches (first word of `kernel`)."""
     import glob
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_summary_cfg{config}.json")), reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            if d.get("log2n") == log2n and d.get("algo", algo) == algo:
+            if (d.get("log2n") == log2n and d.get("algo", algo) == algo
+                    and d.get("kernel", "") and kernel.split()[0].startswith(d["kernel"])):
                 return d["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
@@ -458,7 +460,7 @@ def main():
                        "kernel": w.kernel, "parallelism": f"channels sharded, independent per GPU x {world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(args.config, args.log2n, w.algo_name),
+                         "traffic": load_traffic(args.config, args.log2n, w.algo_name, w.kernel),
                          "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": w.bytes_per_step,
                          "stream_copy_GBps": round(stream, 1), "frac_of_stream_copy": round(achieved / stream, 4)},
             "parity": {"check": getattr(w, "parity_check", "rel_rms vs the f64 restatement (tolerance 1e-6, IIR 1e-5)"),

@@ -1,0 +1,49 @@
+"""Copy one tools/gpu_round.sh session (gpurun_out/<TAG>_*) into profiles/<round>/:
+bench lines, `rocprofv3 --kernel-trace --stats` kernel summaries and the PMC HBM
+traffic summaries (tools/pmc_summary.py) of each config's dominant kernel.
+
+  python tools/collect_round.py --tag r01c --out profiles/r01
+"""
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = {2: ("fir_ols4096_pk_kernel", "fft"), 3: ("sos_wscan_kernel", "scan"),
+          4: ("decim_poly_kernel", "fma"), 5: ("chan1024_kernel", "chan")}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--tag", required=True)
+    p.add_argument("--out", required=True)
+    p.add_argument("--configs", default="2 3 4 5")
+    a = p.parse_args()
+    g = os.path.join(REPO, "gpurun_out")
+    os.makedirs(a.out, exist_ok=True)
+    for c in map(int, a.configs.split()):
+        log = os.path.join(g, f"{a.tag}_bench_cfg{c}.log")
+        line = [ln for ln in open(log) if ln.startswith("{")][-1]
+        d = json.loads(line)
+        with open(os.path.join(a.out, f"bench_cfg{c}.json"), "w") as f:
+            f.write(line)
+        stats = os.path.join(g, f"{a.tag}_prof_cfg{c}", "run_kernel_stats.csv")
+        if os.path.exists(stats):
+            shutil.copy(stats, os.path.join(a.out, f"kernel_stats_cfg{c}.csv"))
+        fetch = os.path.join(g, f"{a.tag}_pmc_fetch_cfg{c}")
+        write = os.path.join(g, f"{a.tag}_pmc_write_cfg{c}")
+        if c in KERNEL and os.path.isdir(fetch) and os.path.isdir(write):
+            k, algo = KERNEL[c]
+            subprocess.run([sys.executable, os.path.join(REPO, "tools", "pmc_summary.py"), "--config", str(c),
+                            "--kernel", k, "--algo", algo, "--fetch", fetch, "--write", write,
+                            "--algorithmic-bytes", str(d["roofline"]["algorithmic_bytes_per_launch"]),
+                            "--out", a.out], check=True)
+        print(f"cfg{c}: {d['ms_per_step']} ms/step, frac {d['roofline']['frac']}, "
+              f"of copy {d['roofline'].get('frac_of_stream_copy')}")
+
+
+if __name__ == "__main__":
+    main()
