@@ -116,14 +116,15 @@ SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
 /* kernel-variant knobs (performance only; results are identical across values, except
  * SDSP_TUNE_OLS_ABLATE_NOMEM, a profiling ablation that skips HBM traffic and leaves the
  * output unwritten).  Overlap-save defaults: PACKED = 1, WIDE = 1 (16-byte accesses in the
- * packed kernel), SEGS_PER_BLOCK = 16.  DEPTH2 / OCCUPANCY name variants that were measured
- * slower and retired: only 0 is accepted (SDSP_E_UNSUPPORTED otherwise). */
+ * packed kernel), SEGS_PER_BLOCK = 16, SCHEDULE = 2, XCD_ORDER = 1. */
 typedef enum {
     SDSP_TUNE_OLS_WIDE = 1,        /* packed overlap-save: 1 (default) = 16-byte global accesses */
     SDSP_TUNE_OLS_INTERLEAVE = 2,  /* 1 (default): segments interleaved across the persistent grid */
-    SDSP_TUNE_OLS_DEPTH2 = 3,
+    SDSP_TUNE_OLS_SCHEDULE = 3,    /* packed overlap-save HBM issue schedule: 0 loads and stores in one burst per
+                                      segment, 1 two segments of loads in flight, 2 (default) .. 10 spread over the
+                                      segment's phases (kern_fir_ols_pk.hip kLoadAt / kStoreAt tables 1..9) */
     SDSP_TUNE_OLS_ABLATE_NOMEM = 4,
-    SDSP_TUNE_OLS_OCCUPANCY = 5,
+    SDSP_TUNE_OLS_XCD_ORDER = 5,   /* packed overlap-save: 1 (default) = each XCD streams one contiguous part */
     SDSP_TUNE_DECIM_SEG = 6,     /* FMA decimator: outputs per lane group (0 = automatic) */
     SDSP_TUNE_IIR_WAVE_SCAN = 7, /* IIR scan kernel: 0 = block scan, 1 (default) = wave scan with 256-byte chunks,
                                     2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */

@@ -170,11 +170,35 @@ __device__ __forceinline__ int bidx(int r, int c) { return r * 16 + ((((c >> 1) 
 // pairs for dwordx4 stores.  P1 writes and P5 reads LDS column col(t) (a
 // permutation of the columns inside each wave, still conflict-free) and w1 is the
 // table row of col(t); P2..P4 are unchanged.
-template <int H2, int ABL, bool ASM, bool W16, int NT = 0>
+template <int B> struct Buf { static constexpr int value = B; };
+
+// HBM issue schedules of the packed kernel (SCH): hook point of each row-pair chunk.
+// Points: 0 loop head, 1 after P1's LDS writes, 2 after P2's DFT, 3 after P2's LDS
+// writes, 4 after P3's forward DFT and spectrum product, 5 after P3's LDS writes,
+// 6 after P4's DFT, 7 after P4's LDS writes, 8 after P5's LDS reads.
+constexpr int kNumSch = 10;
+constexpr int kLoadAt[kNumSch][8] = {
+    {1, 1, 1, 1, 1, 1, 1, 1}, {0, 0, 1, 1, 3, 3, 5, 5}, {0, 0, 1, 2, 3, 4, 5, 6},
+    {0, 1, 2, 3, 4, 5, 6, 7}, {0, 0, 1, 1, 2, 2, 3, 3}, {0, 0, 0, 0, 1, 1, 1, 1},
+    {0, 0, 0, 0, 1, 1, 3, 3}, {0, 0, 1, 1, 3, 3, 5, 5}, {0, 0, 1, 1, 3, 3, 5, 5},
+    {0, 0, 1, 1, 3, 3, 5, 5}};
+constexpr int kStoreAt[kNumSch][8] = {
+    {1, 1, 1, 1, 1, 1, 1, 1}, {1, 1, 3, 3, 5, 5, 7, 7}, {1, 2, 3, 4, 5, 6, 7, 8},
+    {1, 2, 3, 4, 5, 6, 7, 8}, {1, 2, 3, 4, 5, 6, 7, 8}, {1, 2, 3, 4, 5, 6, 7, 8},
+    {1, 1, 3, 3, 5, 5, 7, 7}, {3, 3, 5, 5, 7, 7, 8, 8}, {1, 1, 1, 1, 5, 5, 5, 5},
+    {2, 2, 4, 4, 6, 6, 8, 8}};
+
+template <int H2, int ABL, bool ASM, bool W16, int NT = 0, int D = 1, int SCH = 0>
 __global__ void __launch_bounds__(256, 2)
 fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const f2* __restrict__ tw1,
                       const f2* __restrict__ tw2, f2* __restrict__ y, long long n, long long seg_lo,
-                      long long seg_hi, long long per) {
+                      long long seg_hi, long long per, long long xm) {
+    static_assert(D == 1 || (D == 2 && W16), "two segments in flight need the 16-byte path");
+    // SCH: issue schedule of the HBM traffic over a segment (tables kLoadAt / kStoreAt:
+    // hook point of each row-pair chunk i of the next segment's loads / the previous
+    // segment's deferred stores).  SCH 0: everything at point 1 (D = 2: stores at the end
+    // of P5 instead).
+    static_assert(SCH == 0 || (W16 && D == 1), "spread schedules: 16-byte path, one segment ahead");
     __shared__ __attribute__((aligned(16))) f2 lds[2 * kRegion];
     f2* const rA = lds;
     f2* const rB = lds + kRegion;
@@ -189,9 +213,13 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
     f2 w1[16], w2[16], Hr[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        w1[k] = tw1[col * 16 + k];
-        w2[k] = tw2[lo4 * 16 + k];
-        Hr[k] = Hs[t * 16 + k];
+        if constexpr (ABL & 16) {  // ablation: no table loads
+            w1[k] = w2[k] = Hr[k] = f2{(float)k, (float)t};
+        } else {
+            w1[k] = tw1[col * 16 + k];
+            w2[k] = tw2[lo4 * 16 + k];
+            Hr[k] = Hs[t * 16 + k];
+        }
     }
     constexpr int V = 4096 - 256 * H2;
     // interior segments [seg_lo, seg_hi): per == 0, interleaved over a persistent
@@ -203,25 +231,37 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         seg = seg_lo + blockIdx.x;
     } else {
         sstep = 1;
-        seg = seg_lo + (long long)blockIdx.x * per;
+        // xm > 0: the dispatcher places workgroup b on XCD b % 8; chunk (b % 8) xm + b / 8
+        // keeps each XCD on one contiguous part of the stream
+        const long long b = xm > 0 ? (long long)(blockIdx.x % 8) * xm + blockIdx.x / 8 : (long long)blockIdx.x;
+        seg = seg_lo + b * per;
         const long long e = seg + per;
         if (e < seg_hi) seg_hi = e;
     }
-    f2 nv[16];      // 8-byte path: lane's column over rows
-    float4 nq[8];   // W16 path: row 2i + up, columns colX, colX + 1
-    auto load = [&](long long sg) {
+    f2 nv[16];         // 8-byte path: lane's column over rows
+    float4 nq[D][8];   // W16 path: row 2i + up, columns colX, colX + 1 (D segments in flight)
+    // rows 2i, 2i + 1 for the i with sel(i)
+    auto load = [&](long long sg, auto bt, auto sel) {
+        constexpr int b = decltype(bt)::value;
         if constexpr (ABL & 1) {
+            if constexpr (W16) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) nv[r] = f2{(float)(t + r), (float)(sg & 1023)};
+                for (int i = 0; i < 8; ++i)
+                    if (sel(i)) nq[b][i] = make_float4((float)(t + i), (float)(sg & 1023), 0.f, 1.f);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) nv[r] = f2{(float)(t + r), (float)(sg & 1023)};
+            }
         } else if constexpr (W16) {
             const float4* xb = reinterpret_cast<const float4*>(x + sg * V - 256 * H2 + 256 * up + colX);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
+                if (!sel(i)) continue;
                 if constexpr (NT & 1) {
                     const f4v q = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(xb + 256 * i));
-                    nq[i] = make_float4(q.x, q.y, q.z, q.w);
+                    nq[b][i] = make_float4(q.x, q.y, q.z, q.w);
                 } else {
-                    nq[i] = xb[256 * i];
+                    nq[b][i] = xb[256 * i];
                 }
             }
         } else {
@@ -230,16 +270,21 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
             for (int r = 0; r < 16; ++r) nv[r] = xb[256 * r];
         }
     };
-    // Stores are deferred by one segment: segment s's outputs go out after P1 of
-    // segment s + 1, ahead of the loads for segment s + 2, so the wait for those
-    // loads at the loop head never covers freshly issued stores.
+    // D = 1: stores are deferred by one segment: segment s's outputs go out after P1
+    // of segment s + 1, ahead of the loads for segment s + 2, so the wait for those
+    // loads at the loop head never covers freshly issued stores.  D = 2: the loads
+    // consumed at a loop head were issued two segments earlier, ahead of every
+    // store still in flight, so stores go out at the end of P5 (ov is not kept live
+    // across the next segment).
+    constexpr bool DEFER = D == 1;
     f2 ov[16];
     long long oseg = -1;
-    auto store_out = [&] {
+    auto store_out = [&](auto sel) {
         if constexpr (W16 && !(ABL & 1)) {
             float4* yb = reinterpret_cast<float4*>(y + oseg * V - 256 * H2 + 256 * up + colX);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
+                if (!sel(i)) continue;
                 if (2 * i + 1 < H2) continue;  // both rows are halo
                 float4 q = make_float4(ov[2 * i].x, ov[2 * i].y, ov[2 * i + 1].x, ov[2 * i + 1].y);
                 swap16(q.x, q.z);
@@ -253,8 +298,8 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
             f2* yb = y + oseg * V - 256 * H2 + t;
 #pragma unroll
             for (int k = H2; k < 16; ++k) {
-                if constexpr (ABL & 1) {
-                    if (ov[k].x == 1234.5678f) yb[256 * k] = ov[k];
+                if constexpr (ABL & 1) {  // keep the outputs live, no stores
+                    if (sel(k >> 1)) { const f2 tv = ov[k]; asm volatile("" : : "v"(tv)); }
                 } else {
                     yb[256 * k] = ov[k];
                 }
@@ -278,15 +323,17 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         if constexpr (ABL & 4) return tmp[k];
         else return r[i];
     };
-    if (seg < seg_hi) load(seg);
-    for (; seg < seg_hi; seg += sstep) {
+    // one segment; its input sits in buffer b (nq[b] / nv), the load it issues
+    // (segment seg + D * sstep, clamped) refills the same buffer
+    auto segment = [&](auto bt) {
+        constexpr int b = decltype(bt)::value;
 #pragma unroll
         for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(w1[k]), "+v"(w2[k]), "+v"(Hr[k]));
         f2 v[16];
-        if constexpr (W16 && !(ABL & 1)) {
+        if constexpr (W16) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                float4 q = nq[i];
+                float4 q = nq[b][i];
                 swap16(q.x, q.z);
                 swap16(q.y, q.w);
                 v[2 * i] = f2{q.x, q.y};
@@ -296,30 +343,42 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
 #pragma unroll
             for (int r = 0; r < 16; ++r) v[r] = nv[r];
         }
-        const long long nxt = seg + sstep < seg_hi ? seg + sstep : seg;
-        if constexpr (ABL == 8) {  // the kernel's HBM traffic alone: same grid, loads and deferred stores
+        const long long ahead = seg + D * sstep;
+        const long long nxt = ahead < seg_hi ? ahead : seg;
+        // HBM traffic issued at hook point P (SCH tables)
+        auto hook = [&](auto pt) {
+            constexpr int P = decltype(pt)::value;
+            if constexpr (DEFER) {
+                if (oseg >= 0) store_out([](int i) { return kStoreAt[SCH][i] == P; });
+            }
+            load(nxt, bt, [](int i) { return kLoadAt[SCH][i] == P; });
+        };
+        hook(Buf<0>{});
+        if constexpr ((ABL & ~16) == 8) {  // the kernel's HBM traffic alone: same grid, loads and deferred stores
 #pragma unroll
             for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[k]));
-            if (oseg >= 0) store_out();
-            load(nxt);
+            if (DEFER && oseg >= 0) store_out([](int) { return true; });
+            load(nxt, bt, [](int) { return true; });
 #pragma unroll
             for (int k = 0; k < 16; ++k) ov[k] = v[k];
             oseg = seg;
-            continue;
+            if constexpr (!DEFER) store_out([](int) { return true; });
+            return;
         }
         // P1: DFT over n2 -> k0, twiddle, A[k0][t]
         pdft16<false>(v);
 #pragma unroll
         for (int k = 0; k < 16; ++k) sto(rA, k * kRowA + col, k, pmul<ASM>(v[kout(k)], w1[k]));
-        if (oseg >= 0) store_out();
-        load(nxt);
+        hook(Buf<1>{});
         bar();
         // P2: lane (k0=hi4, n0=lo4) reads n1
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = ldo(rA, hi4 * kRowA + 16 * k + lo4, k);
         pdft16<false>(v);
+        hook(Buf<2>{});
 #pragma unroll
         for (int k = 0; k < 16; ++k) sto(rB, bidx(16 * hi4 + k, lo4), k, pmul<ASM>(v[kout(k)], w2[k]));
+        hook(Buf<3>{});
         bar();
         // P3: lane (k0=hi4, k1=lo4) reads its row over n0
         {
@@ -340,40 +399,64 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         f2 u[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) u[k] = pmul<ASM>(v[kout(k)], Hr[k]);
+        hook(Buf<4>{});
         pdft16<true>(u);
         {
             float4* row = reinterpret_cast<float4*>(rA + t * 16);
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
                 const f2 a = pmulc<ASM>(u[kout(2 * p)], w2[2 * p]);
-                const f2 b = pmulc<ASM>(u[kout(2 * p + 1)], w2[2 * p + 1]);
+                const f2 c = pmulc<ASM>(u[kout(2 * p + 1)], w2[2 * p + 1]);
                 if constexpr (ABL & 4) {
                     tmp[2 * p] = a;
-                    tmp[2 * p + 1] = b;
+                    tmp[2 * p + 1] = c;
                 } else {
-                    row[(p ^ (t >> 1)) & 7] = make_float4(a.x, a.y, b.x, b.y);
+                    row[(p ^ (t >> 1)) & 7] = make_float4(a.x, a.y, c.x, c.y);
                 }
             }
         }
+        hook(Buf<5>{});
         bar();
         // P4: lane (k0=hi4, n0=lo4) reads k1
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = ldo(rA, bidx(16 * hi4 + k, lo4), k);
         pdft16<true>(v);
+        hook(Buf<6>{});
 #pragma unroll
         for (int k = 0; k < 16; ++k) sto(rB, hi4 * kRowA + 16 * k + lo4, k, v[kout(k)]);
+        hook(Buf<7>{});
         bar();
         // P5: lane t=(n1,n0) reads k0
 #pragma unroll
         for (int k = 0; k < 16; ++k) v[k] = pmulc<ASM>(ldo(rB, k * kRowA + col, k), w1[k]);
+        hook(Buf<8>{});
         pdft16<true>(v);
 #pragma unroll
         for (int k = 0; k < 16; ++k) ov[k] = v[kout(k)];
         oseg = seg;
+        if constexpr (!DEFER) store_out([](int) { return true; });
         // the next segment's P1 writes region A: every lane has finished reading
         // region A (P4) before the barrier that precedes P5.
+    };
+    if constexpr (D == 1) {
+        if (seg < seg_hi)
+            load(seg, Buf<0>{}, [](int) { return true; });
+        for (; seg < seg_hi; seg += sstep) segment(Buf<0>{});
+    } else {
+        // two buffers: the loop body is unrolled so each buffer index is static
+        if (seg < seg_hi) {
+            load(seg, Buf<0>{}, [](int) { return true; });
+            load(seg + sstep < seg_hi ? seg + sstep : seg, Buf<1>{}, [](int) { return true; });
+        }
+        while (seg < seg_hi) {
+            segment(Buf<0>{});
+            seg += sstep;
+            if (seg >= seg_hi) break;
+            segment(Buf<1>{});
+            seg += sstep;
+        }
     }
-    if (oseg >= 0) store_out();
+    if (DEFER && oseg >= 0) store_out([](int) { return true; });
 }
 
 hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, int num_cus,
@@ -384,12 +467,19 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
     const bool w16 = p.wide && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0 &&
                      (channels == 1 || n % 2 == 0);
     long long blocks = (long long)num_cus * 2;
-    if (per > 0) blocks = (hi - lo + per - 1) / per;
+    long long xm = 0;
+    if (per > 0) {
+        blocks = (hi - lo + per - 1) / per;
+        if (p.xcd) {
+            xm = (blocks + 7) / 8;
+            blocks = 8 * xm;
+        }
+    }
     else if (blocks > hi - lo) blocks = hi - lo;
     dim3 grid((unsigned)blocks, (unsigned)channels);
 #define SDSP_OLS_PK_W(HV, A, M, W)                                                                               \
     hipLaunchKernelGGL((fir_ols4096_pk_kernel<HV, A, M, W>), grid, dim3(256), 0, s, (const f2*)x, (const f2*)p.d_H, \
-                       (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per)
+                       (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per, xm)
 #define SDSP_OLS_PK_L(HV, A)                                                                                     \
     do {                                                                                                         \
         if (p.packed % 2 == 0) {                                                                                 \
@@ -399,10 +489,48 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
         }                                                                                                        \
     } while (0)
 #define SDSP_OLS_PK(HV) SDSP_OLS_PK_L(HV, 0)
+    if (w16 && p.depth2 && p.halo_rows == 1) {  // loads two segments ahead and / or spread over the phases
+#define SDSP_OLS_PK_D2(M, A, DV, SPV, NTV)                                                                       \
+    hipLaunchKernelGGL((fir_ols4096_pk_kernel<1, A, M, true, NTV, DV, SPV>), grid, dim3(256), 0, s, (const f2*)x, \
+                       (const f2*)p.d_H, (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per, xm)
+#define SDSP_OLS_PK_D2A(A, DV, SPV)                                                                              \
+    do {                                                                                                         \
+        if (DV == 1 && SPV == 1 && (p.nt & 3) == 2 && !A) SDSP_OLS_PK_D2(true, 0, 1, 1, 2);                      \
+        else if (DV == 1 && SPV == 1 && (p.nt & 3) == 3 && !A) SDSP_OLS_PK_D2(true, 0, 1, 1, 3);                 \
+        else if (DV == 1 && SPV == 1 && (p.nt & 3) == 1 && !A) SDSP_OLS_PK_D2(true, 0, 1, 1, 1);                 \
+        else if (p.packed % 2 != 0) SDSP_OLS_PK_D2(true, A, DV, SPV, 0);                                         \
+        else SDSP_OLS_PK_D2(false, A, DV, SPV, 0);                                                               \
+    } while (0)
+#define SDSP_OLS_PK_D2V(A)                                                                                       \
+    do {                                                                                                         \
+        switch (p.depth2) {                                                                                      \
+            case 1: SDSP_OLS_PK_D2A(A, 2, 0); break;                                                             \
+            case 2: SDSP_OLS_PK_D2A(A, 1, 1); break;                                                             \
+            case 3: SDSP_OLS_PK_D2A(A, 1, 2); break;                                                             \
+            case 4: SDSP_OLS_PK_D2A(A, 1, 3); break;                                                             \
+            case 5: SDSP_OLS_PK_D2A(A, 1, 4); break;                                                             \
+            case 6: SDSP_OLS_PK_D2A(A, 1, 5); break;                                                             \
+            case 7: SDSP_OLS_PK_D2A(A, 1, 6); break;                                                             \
+            case 8: SDSP_OLS_PK_D2A(A, 1, 7); break;                                                             \
+            case 9: SDSP_OLS_PK_D2A(A, 1, 8); break;                                                             \
+            default: SDSP_OLS_PK_D2A(A, 1, 9); break;                                                            \
+        }                                                                                                        \
+    } while (0)
+        switch (ablate) {
+            case 0: SDSP_OLS_PK_D2V(0); break;
+            case 1: SDSP_OLS_PK_D2V(1); break;
+            case 8: SDSP_OLS_PK_D2V(8); break;
+            default: return hipErrorInvalidValue;
+        }
+#undef SDSP_OLS_PK_D2V
+#undef SDSP_OLS_PK_D2A
+#undef SDSP_OLS_PK_D2
+        return hipGetLastError();
+    }
     if (w16 && p.nt && p.halo_rows == 1 && !ablate) {  // nontemporal hints (bit 0 loads, bit 1 stores), h2 = 1
 #define SDSP_OLS_PK_NT(M, NTV)                                                                                   \
     hipLaunchKernelGGL((fir_ols4096_pk_kernel<1, 0, M, true, NTV>), grid, dim3(256), 0, s, (const f2*)x,         \
-                       (const f2*)p.d_H, (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per)
+                       (const f2*)p.d_H, (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per, xm)
         const int ntv = p.nt & 3;
         if (p.packed % 2 == 0) {
             if (ntv == 1) SDSP_OLS_PK_NT(false, 1); else if (ntv == 2) SDSP_OLS_PK_NT(false, 2); else SDSP_OLS_PK_NT(false, 3);
@@ -418,6 +546,7 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
         else if (ablate == 3) SDSP_OLS_PK_L(1, 3);
         else if (ablate == 7) SDSP_OLS_PK_L(1, 7);
         else if (ablate == 8) SDSP_OLS_PK_L(1, 8);
+        else if (ablate == 24) SDSP_OLS_PK_L(1, 24);
         else return hipErrorInvalidValue;
         return hipGetLastError();
     }

@@ -97,7 +97,9 @@ struct sdsp_fir {
     DevBuf stage_in, stage_out;
     // overlap-save plan
     bool ols_ok = false;
-    bool ols_wide = true, ols_interleave = true, ols_depth2 = false;
+    bool ols_wide = true, ols_interleave = true;
+    int ols_depth2 = 2;  // SDSP_TUNE_OLS_SCHEDULE
+    bool ols_xcd = true;  // SDSP_TUNE_OLS_XCD_ORDER
     int ols_nomem = 0;
     int ols_nt = 0;
     int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
@@ -212,6 +214,7 @@ int ols_build(sdsp_fir* h) {
     h->ols.wave = h->ols_wave && hr1k > 0;
     h->ols.packed = h->ols_packed;
     h->ols.segs_per_block = h->ols_segs;
+    h->ols.xcd = h->ols_xcd;
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -350,22 +353,24 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     switch (key) {
         // retired overlap-save variants (measured slower): only their default is accepted
         case SDSP_TUNE_OLS_WIDE: h->ols_wide = value != 0; break;  // packed kernel only
-        case SDSP_TUNE_OLS_DEPTH2:
-        case SDSP_TUNE_OLS_OCCUPANCY:
-            if (value != 0) return SDSP_E_UNSUPPORTED;
+        case SDSP_TUNE_OLS_SCHEDULE:  // packed kernel, 16-byte rows, h2 = 1
+            if (value < 0 || value > 10) return SDSP_E_INVALID_ARGUMENT;
+            h->ols_depth2 = value;
             break;
+        case SDSP_TUNE_OLS_XCD_ORDER: h->ols_xcd = value != 0; break;
         case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
         case SDSP_TUNE_OLS_NONTEMPORAL: h->ols_nt = value & 7; break;
         case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
         case SDSP_TUNE_OLS_SEGS_PER_BLOCK: h->ols_segs = value > 0 ? value : 0; break;
         case SDSP_TUNE_OLS_PACKED: h->ols_packed = (value >= 0 && value <= 6) ? value : 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 7) ? value : 0; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 8) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }
     h->ols.wide = h->ols_wide;
     h->ols.interleave = h->ols_interleave;
     h->ols.depth2 = h->ols_depth2;
+    h->ols.xcd = h->ols_xcd;
     h->ols.nomem = h->ols_nomem;
     h->ols.nt = h->ols_nt;
     h->ols.occ = h->ols_occ;

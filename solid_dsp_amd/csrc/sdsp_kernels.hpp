@@ -35,7 +35,8 @@ struct OlsPlan {
     int halo_rows;  // h2: halo = 256*h2 >= L-1
     bool wide;        // 16-byte lane-pair global loads/stores
     bool interleave;  // segment order across the persistent grid
-    bool depth2;      // two segments of loads in flight (8-byte path)
+    int depth2;       // packed kernel (16-byte rows, h2 = 1) HBM issue schedule: 0 default, 1 two segments of
+                      // loads in flight, 2..6 one segment with the SCH tables 1..5 of kern_fir_ols_pk.hip
     int nomem;        // profiling ablation (outputs invalid): 1 no HBM traffic, 2 no loads, 3 no stores,
                       // 4 no HBM + no barriers; packed kernel: 5 no HBM + no barriers, 6 also no LDS,
                       // 7 HBM traffic only
@@ -49,6 +50,7 @@ struct OlsPlan {
     int packed = 0;  // packed-FP32 interior kernel (kern_fir_ols_pk.hip): odd = asm table products, even = compiler-
                      // visible; 1-2 default scheduler, 3-4 max-ilp, 5-6 iterative-ilp
     int segs_per_block = 0;  // packed kernel: 0 persistent interleaved grid, > 0 consecutive segments per workgroup
+    bool xcd = true;         // packed kernel, segs_per_block > 0: workgroup b % 8 (its XCD) takes a contiguous 1/8 of the chunks
 };
 constexpr int kOlsN = 4096;
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,

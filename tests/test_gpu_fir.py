@@ -180,6 +180,27 @@ def test_fir_fft_packed_kernel_bit_identical(L, pk, per, wide, ch):
     assert rel_rms(y[-1] if ch > 1 else y, ref) <= 1e-6
 
 
+@pytest.mark.parametrize("sched,xcd,per", [(v, 1, 16) for v in range(11)] + [(2, 0, 16), (2, 1, 3), (10, 1, 1)])
+@pytest.mark.parametrize("ch", [1, 2])
+def test_fir_fft_packed_schedules_bit_identical(sched, xcd, per, ch):
+    # HBM issue schedules (SDSP_TUNE_OLS_SCHEDULE = 3: burst / two segments ahead / spread over
+    # the phases) and the XCD-contiguous chunk order (SDSP_TUNE_OLS_XCD_ORDER = 5) only move
+    # loads and stores: bits equal the scalar overlap-save kernel across ragged calls
+    h = _f32_taps(256, 0.1)
+    x = O.synth(20250228, 5, 0, 400000 * ch, complex_=True)
+    x = x.reshape(ch, -1) if ch > 1 else x
+    a = FIRFilter(h, F32(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
+    b = FIRFilter(h, F32(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
+    assert sd.lib().sdsp_fir_set_tuning(a._h, 3, sched) == 0
+    assert sd.lib().sdsp_fir_set_tuning(a._h, 5, xcd) == 0
+    assert sd.lib().sdsp_fir_set_tuning(a._h, 13, per) == 0
+    assert sd.lib().sdsp_fir_set_tuning(b._h, 12, 0) == 0
+    cuts = [0, 5, 4000, 123457, 400000]
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        xa = x[..., lo:hi]
+        assert bits_equal(a.execute_block(xa), b.execute_block(xa)), (sched, xcd, per, ch, lo, hi)
+
+
 def test_fir_fft_matches_exact_kernel_across_calls():
     h = _f32_taps(256, 0.1)
     x = O.synth(7, 3, 0, 200000, complex_=True)

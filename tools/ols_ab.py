@@ -9,7 +9,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(rounds=8, log2n=30):
+def main(rounds=int(os.environ.get("OLS_ROUNDS", "12")), log2n=30):
     import torch
     import solid_dsp_amd as sd
     from solid_dsp_amd import FIRFilter
@@ -20,10 +20,10 @@ def main(rounds=8, log2n=30):
     sd.lib().sdsp_synth_f32_device(d_in.data_ptr(), 20250226, 0, 0, 2 * n, None)
     outs = {}
     variants = {}
-    cfgs = json.loads(os.environ.get("OLS_VARIANTS", "[[0,1,0,0],[0,1,0,1]]"))
+    cfgs = json.loads(os.environ.get("OLS_VARIANTS", "[[1,1,2,0,1,0,0,1,16],[1,1,2,1,1,0,0,1,16]]"))
     for cfg in cfgs:
         wide, inter, d2, nomem = cfg[:4]
-        occ = cfg[4] if len(cfg) > 4 else 0
+        xcd = cfg[4] if len(cfg) > 4 else 1
         nt = cfg[5] if len(cfg) > 5 else 0
         wave = cfg[6] if len(cfg) > 6 else 0
         pk = cfg[7] if len(cfg) > 7 else 0
@@ -33,12 +33,12 @@ def main(rounds=8, log2n=30):
         sd.lib().sdsp_fir_set_tuning(f._h, 2, inter)
         sd.lib().sdsp_fir_set_tuning(f._h, 3, d2)
         sd.lib().sdsp_fir_set_tuning(f._h, 4, nomem)
-        sd.lib().sdsp_fir_set_tuning(f._h, 5, occ)
+        sd.lib().sdsp_fir_set_tuning(f._h, 5, xcd)
         sd.lib().sdsp_fir_set_tuning(f._h, 10, nt)
         sd.lib().sdsp_fir_set_tuning(f._h, 11, wave)
         sd.lib().sdsp_fir_set_tuning(f._h, 12, pk)
         sd.lib().sdsp_fir_set_tuning(f._h, 13, per)
-        variants[f"wave{wave}_pk{pk}_per{per}_w{wide}_inter{inter}_nt{nt}_nomem{nomem}"] = f
+        variants[f"wave{wave}_pk{pk}_per{per}_sch{d2}_xcd{xcd}_w{wide}_inter{inter}_nt{nt}_nomem{nomem}"] = f
     s = torch.cuda.current_stream()
     times = {k: [] for k in variants}
     for k, f in variants.items():
@@ -57,8 +57,11 @@ def main(rounds=8, log2n=30):
         return float(np.linalg.norm(a - b) / np.linalg.norm(b))
     same = {k: agree(v) for k, v in outs.items()}
     d_out = torch.empty_like(d_in)
+    order = list(variants.items())
+    rng = np.random.default_rng(1)
     for r in range(rounds):
-        for k, f in variants.items():
+        rng.shuffle(order)  # a different variant order every round
+        for k, f in order:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             f.execute_block_device(d_in, n, d_out, s)
