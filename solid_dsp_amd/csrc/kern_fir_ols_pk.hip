@@ -151,8 +151,17 @@ template <bool INV> __device__ __forceinline__ void pdft16(f2 (&v)[16]) {
 
 constexpr int kRowA = 272;           // A image: 16 rows of 256 (+16 pad) samples
 constexpr int kRegion = 16 * kRowA;  // samples per LDS region
-// B image: 256 rows x 16 samples, pairs XOR-swizzled by (row>>1)&7
-__device__ __forceinline__ int bidx(int r, int c) { return r * 16 + ((((c >> 1) ^ (r >> 1)) & 7) << 1) + (c & 1); }
+// LDS images, bank-conflict free for every access of P1..P5 (MI355X_MICROARCH.md §LDS
+// lane groups):
+// A image: 16 rows of 256 (+16 pad) samples; column c sits at acol(c) = c ^ bit 4 of c,
+//   so P1's 16-lane ds_write_b64 groups (columns 0, 2, .., 30 of the W16 lane order)
+//   cover all 32 write banks
+// B image: 256 rows x 16 samples; row r sits at physical row r ^ bit 4 of r (rows r and
+//   r + 16, read by one 32-lane half in P4, land in opposite halves of the 64 banks) and its
+//   16-byte pairs are XOR-swizzled by r & 7 (P3's 8-lane ds_write_b128 groups hit 8 slots)
+__device__ __forceinline__ int acol(int c) { return c ^ ((c >> 4) & 1); }
+__device__ __forceinline__ int brow(int r) { return r ^ ((r >> 4) & 1); }
+__device__ __forceinline__ int bidx(int r, int c) { return brow(r) * 16 + ((((c >> 1) ^ r) & 7) << 1) + (c & 1); }
 
 }  // namespace
 
@@ -229,6 +238,16 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
     if (per == 0) {
         sstep = gridDim.x;
         seg = seg_lo + blockIdx.x;
+    } else if (per < 0) {
+        // XCD-local interleave: XCD b % 8 owns one contiguous eighth of the segments and its
+        // resident workgroups b / 8 walk it interleaved (a compact window per XCD; the halo
+        // row of a segment was read by a neighbour on the same XCD, i.e. through its L2)
+        const long long x8 = blockIdx.x % 8, nj = gridDim.x / 8;
+        const long long s8 = (seg_hi - seg_lo + 7) / 8;
+        const long long a = seg_lo + x8 * s8;
+        if (a + s8 < seg_hi) seg_hi = a + s8;
+        seg = a + blockIdx.x / 8;
+        sstep = nj;
     } else {
         sstep = 1;
         // xm > 0: the dispatcher places workgroup b on XCD b % 8; chunk (b % 8) xm + b / 8
@@ -368,12 +387,12 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         // P1: DFT over n2 -> k0, twiddle, A[k0][t]
         pdft16<false>(v);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) sto(rA, k * kRowA + col, k, pmul<ASM>(v[kout(k)], w1[k]));
+        for (int k = 0; k < 16; ++k) sto(rA, k * kRowA + acol(col), k, pmul<ASM>(v[kout(k)], w1[k]));
         hook(Buf<1>{});
         bar();
         // P2: lane (k0=hi4, n0=lo4) reads n1
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = ldo(rA, hi4 * kRowA + 16 * k + lo4, k);
+        for (int k = 0; k < 16; ++k) v[k] = ldo(rA, hi4 * kRowA + 16 * k + (lo4 ^ (k & 1)), k);
         pdft16<false>(v);
         hook(Buf<2>{});
 #pragma unroll
@@ -382,14 +401,14 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         bar();
         // P3: lane (k0=hi4, k1=lo4) reads its row over n0
         {
-            const float4* row = reinterpret_cast<const float4*>(rB + t * 16);
+            const float4* row = reinterpret_cast<const float4*>(rB + brow(t) * 16);
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
                 if constexpr (ABL & 4) {
                     v[2 * p] = tmp[2 * p];
                     v[2 * p + 1] = tmp[2 * p + 1];
                 } else {
-                    const float4 q = row[(p ^ (t >> 1)) & 7];
+                    const float4 q = row[(p ^ t) & 7];
                     v[2 * p] = f2{q.x, q.y};
                     v[2 * p + 1] = f2{q.z, q.w};
                 }
@@ -402,7 +421,7 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         hook(Buf<4>{});
         pdft16<true>(u);
         {
-            float4* row = reinterpret_cast<float4*>(rA + t * 16);
+            float4* row = reinterpret_cast<float4*>(rA + brow(t) * 16);
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
                 const f2 a = pmulc<ASM>(u[kout(2 * p)], w2[2 * p]);
@@ -411,7 +430,7 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
                     tmp[2 * p] = a;
                     tmp[2 * p + 1] = c;
                 } else {
-                    row[(p ^ (t >> 1)) & 7] = make_float4(a.x, a.y, c.x, c.y);
+                    row[(p ^ t) & 7] = make_float4(a.x, a.y, c.x, c.y);
                 }
             }
         }
@@ -423,12 +442,12 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         pdft16<true>(v);
         hook(Buf<6>{});
 #pragma unroll
-        for (int k = 0; k < 16; ++k) sto(rB, hi4 * kRowA + 16 * k + lo4, k, v[kout(k)]);
+        for (int k = 0; k < 16; ++k) sto(rB, hi4 * kRowA + 16 * k + (lo4 ^ (k & 1)), k, v[kout(k)]);
         hook(Buf<7>{});
         bar();
         // P5: lane t=(n1,n0) reads k0
 #pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = pmulc<ASM>(ldo(rB, k * kRowA + col, k), w1[k]);
+        for (int k = 0; k < 16; ++k) v[k] = pmulc<ASM>(ldo(rB, k * kRowA + acol(col), k), w1[k]);
         hook(Buf<8>{});
         pdft16<true>(v);
 #pragma unroll
@@ -475,6 +494,7 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
             blocks = 8 * xm;
         }
     }
+    else if (per < 0) blocks = blocks / 8 * 8;  // grid must be a multiple of the 8 XCDs
     else if (blocks > hi - lo) blocks = hi - lo;
     dim3 grid((unsigned)blocks, (unsigned)channels);
 #define SDSP_OLS_PK_W(HV, A, M, W)                                                                               \
