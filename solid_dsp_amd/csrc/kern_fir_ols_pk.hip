@@ -220,16 +220,30 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
     const int colX = 32 * (t >> 5) + 2 * (t & 15);  // W16: first column of the lane pair
     const int col = W16 ? colX + up : t;
     f2 w1[16], w2[16], Hr[16];
+    // issued after the first segment's loads: a one-shot workgroup (per = 1) then waits
+    // for the tables only where P1 first needs them, not ahead of its HBM stream
+    auto load_tables = [&] {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if constexpr (ABL & 16) {  // ablation: no table loads
-            w1[k] = w2[k] = Hr[k] = f2{(float)k, (float)t};
-        } else {
-            w1[k] = tw1[col * 16 + k];
-            w2[k] = tw2[lo4 * 16 + k];
-            Hr[k] = Hs[t * 16 + k];
+        for (int k = 0; k < 16; ++k) {
+            if constexpr (ABL & 16) {  // ablation: no table loads
+                w1[k] = w2[k] = Hr[k] = f2{(float)k, (float)t};
+            } else if constexpr (ABL & 32) {  // ablation: the spectrum table only
+                w1[k] = w2[k] = f2{(float)k, (float)t};
+                const float4 e = reinterpret_cast<const float4*>(Hs)[(k / 2) * 256 + t];
+                Hr[k] = k % 2 ? f2{e.z, e.w} : f2{e.x, e.y};
+            } else if (k % 2 == 0) {  // k-pair major tables (OlsPlan::d_pkt): coalesced 16-byte loads
+                const float4 a = reinterpret_cast<const float4*>(tw1)[(k / 2) * 256 + col];
+                const float4 c = reinterpret_cast<const float4*>(tw2)[(k / 2) * 16 + lo4];
+                const float4 e = reinterpret_cast<const float4*>(Hs)[(k / 2) * 256 + t];
+                w1[k] = f2{a.x, a.y};
+                w1[k + 1] = f2{a.z, a.w};
+                w2[k] = f2{c.x, c.y};
+                w2[k + 1] = f2{c.z, c.w};
+                Hr[k] = f2{e.x, e.y};
+                Hr[k + 1] = f2{e.z, e.w};
+            }
         }
-    }
+    };
     constexpr int V = 4096 - 256 * H2;
     // interior segments [seg_lo, seg_hi): per == 0, interleaved over a persistent
     // grid; per > 0, `per` consecutive segments per workgroup (the dispatcher then
@@ -346,8 +360,6 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
     // (segment seg + D * sstep, clamped) refills the same buffer
     auto segment = [&](auto bt) {
         constexpr int b = decltype(bt)::value;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(w1[k]), "+v"(w2[k]), "+v"(Hr[k]));
         f2 v[16];
         if constexpr (W16) {
 #pragma unroll
@@ -372,10 +384,11 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
             }
             load(nxt, bt, [](int i) { return kLoadAt[SCH][i] == P; });
         };
-        hook(Buf<0>{});
-        if constexpr ((ABL & ~16) == 8) {  // the kernel's HBM traffic alone: same grid, loads and deferred stores
+        if constexpr ((ABL & ~48) == 8) {  // the kernel's HBM traffic alone: same grid, loads and deferred stores
 #pragma unroll
             for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(v[k]));
+#pragma unroll
+            for (int k = 0; k < 16; ++k) asm volatile("" : : "v"(w1[k]), "v"(w2[k]), "v"(Hr[k]));
             if (DEFER && oseg >= 0) store_out([](int) { return true; });
             load(nxt, bt, [](int) { return true; });
 #pragma unroll
@@ -384,6 +397,7 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
             if constexpr (!DEFER) store_out([](int) { return true; });
             return;
         }
+        hook(Buf<0>{});
         // P1: DFT over n2 -> k0, twiddle, A[k0][t]
         pdft16<false>(v);
 #pragma unroll
@@ -454,12 +468,16 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
         for (int k = 0; k < 16; ++k) ov[k] = v[kout(k)];
         oseg = seg;
         if constexpr (!DEFER) store_out([](int) { return true; });
+        // tables opaque once per segment: swizzled copies of them are not hoisted out of the loop
+#pragma unroll
+        for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(w1[k]), "+v"(w2[k]), "+v"(Hr[k]));
         // the next segment's P1 writes region A: every lane has finished reading
         // region A (P4) before the barrier that precedes P5.
     };
     if constexpr (D == 1) {
         if (seg < seg_hi)
             load(seg, Buf<0>{}, [](int) { return true; });
+        load_tables();
         for (; seg < seg_hi; seg += sstep) segment(Buf<0>{});
     } else {
         // two buffers: the loop body is unrolled so each buffer index is static
@@ -467,6 +485,7 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
             load(seg, Buf<0>{}, [](int) { return true; });
             load(seg + sstep < seg_hi ? seg + sstep : seg, Buf<1>{}, [](int) { return true; });
         }
+        load_tables();
         while (seg < seg_hi) {
             segment(Buf<0>{});
             seg += sstep;
@@ -480,6 +499,9 @@ fir_ols4096_pk_kernel(const f2* __restrict__ x, const f2* __restrict__ Hs, const
 
 hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, int num_cus,
                              hipStream_t s, long long lo, long long hi, int ablate) {
+    // k-pair-major tables (OlsPlan::d_pkt): spectrum, tw1, tw2 parts
+    const float4* const pkt = reinterpret_cast<const float4*>(p.d_pkt);
+#define PK_TABLES (const f2*)pkt, (const f2*)(pkt + 2048), (const f2*)(pkt + 4096)
     if (hi <= lo) return hipSuccess;
     const long long per = p.segs_per_block;
     // 16-byte accesses need 16-byte aligned rows in every channel
@@ -498,8 +520,8 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
     else if (blocks > hi - lo) blocks = hi - lo;
     dim3 grid((unsigned)blocks, (unsigned)channels);
 #define SDSP_OLS_PK_W(HV, A, M, W)                                                                               \
-    hipLaunchKernelGGL((fir_ols4096_pk_kernel<HV, A, M, W>), grid, dim3(256), 0, s, (const f2*)x, (const f2*)p.d_H, \
-                       (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per, xm)
+    hipLaunchKernelGGL((fir_ols4096_pk_kernel<HV, A, M, W>), grid, dim3(256), 0, s, (const f2*)x, PK_TABLES,      \
+                       (f2*)y, (long long)n, lo, hi, per, xm)
 #define SDSP_OLS_PK_L(HV, A)                                                                                     \
     do {                                                                                                         \
         if (p.packed % 2 == 0) {                                                                                 \
@@ -512,7 +534,7 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
     if (w16 && p.depth2 && p.halo_rows == 1) {  // loads two segments ahead and / or spread over the phases
 #define SDSP_OLS_PK_D2(M, A, DV, SPV, NTV)                                                                       \
     hipLaunchKernelGGL((fir_ols4096_pk_kernel<1, A, M, true, NTV, DV, SPV>), grid, dim3(256), 0, s, (const f2*)x, \
-                       (const f2*)p.d_H, (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per, xm)
+                       PK_TABLES, (f2*)y, (long long)n, lo, hi, per, xm)
 #define SDSP_OLS_PK_D2A(A, DV, SPV)                                                                              \
     do {                                                                                                         \
         if (DV == 1 && SPV == 1 && (p.nt & 3) == 2 && !A) SDSP_OLS_PK_D2(true, 0, 1, 1, 2);                      \
@@ -540,6 +562,9 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
             case 0: SDSP_OLS_PK_D2V(0); break;
             case 1: SDSP_OLS_PK_D2V(1); break;
             case 8: SDSP_OLS_PK_D2V(8); break;
+            case 24: SDSP_OLS_PK_D2V(24); break;
+            case 40: SDSP_OLS_PK_D2V(40); break;
+            case 56: SDSP_OLS_PK_D2V(56); break;
             default: return hipErrorInvalidValue;
         }
 #undef SDSP_OLS_PK_D2V
@@ -550,7 +575,7 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
     if (w16 && p.nt && p.halo_rows == 1 && !ablate) {  // nontemporal hints (bit 0 loads, bit 1 stores), h2 = 1
 #define SDSP_OLS_PK_NT(M, NTV)                                                                                   \
     hipLaunchKernelGGL((fir_ols4096_pk_kernel<1, 0, M, true, NTV>), grid, dim3(256), 0, s, (const f2*)x,         \
-                       (const f2*)p.d_H, (const f2*)p.d_tw1, (const f2*)p.d_tw2, (f2*)y, (long long)n, lo, hi, per, xm)
+                       PK_TABLES, (f2*)y, (long long)n, lo, hi, per, xm)
         const int ntv = p.nt & 3;
         if (p.packed % 2 == 0) {
             if (ntv == 1) SDSP_OLS_PK_NT(false, 1); else if (ntv == 2) SDSP_OLS_PK_NT(false, 2); else SDSP_OLS_PK_NT(false, 3);
@@ -580,6 +605,7 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
 #undef SDSP_OLS_PK
 #undef SDSP_OLS_PK_L
 #undef SDSP_OLS_PK_W
+#undef PK_TABLES
     return hipGetLastError();
 }
 

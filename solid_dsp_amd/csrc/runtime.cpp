@@ -105,7 +105,7 @@ struct sdsp_fir {
     int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
     int decim_seg = 0;  // outputs per lane group of the polyphase decimator (0 = auto)
     OlsPlan ols{};
-    DevBuf d_H, d_tw1, d_tw2, d_H1k, d_tw1k;
+    DevBuf d_H, d_tw1, d_tw2, d_H1k, d_tw1k, d_pkt;
     bool ols_wave = false;  // wave-per-segment N = 1024 kernel (SDSP_TUNE_OLS_WAVE)
     int ols_segs = 16;  // SDSP_TUNE_OLS_SEGS_PER_BLOCK
     int ols_packed = 1;  // packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED): 0 off, 1..6 builds
@@ -179,6 +179,22 @@ int ols_build(sdsp_fir* h) {
     SDSP_TRY(hipMemcpyAsync(h->d_H.p, Hs.data(), Hs.size() * 4, hipMemcpyHostToDevice, h->stream), "copy H");
     SDSP_TRY(hipMemcpyAsync(h->d_tw1.p, tw1.data(), tw1.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw1");
     SDSP_TRY(hipMemcpyAsync(h->d_tw2.p, tw2.data(), tw2.size() * 4, hipMemcpyHostToDevice, h->stream), "copy tw2");
+    // the same tables for the packed kernel, k-pair major so that a table load is one
+    // coalesced 16-byte access per lane: float4 (p, i) = entries 2p, 2p + 1 of row i;
+    // [0, 2048): H rows t, [2048, 4096): tw1 rows, [4096, 4224): tw2 rows
+    std::vector<float> pkt(4 * 4224);
+    for (int q = 0; q < 8; ++q) {
+        for (int i = 0; i < 256; ++i)
+            for (int e = 0; e < 4; ++e) {
+                pkt[4 * (q * 256 + i) + e] = Hs[2 * (i * 16 + 2 * q) + e];
+                pkt[4 * (2048 + q * 256 + i) + e] = tw1[2 * (i * 16 + 2 * q) + e];
+            }
+        for (int i = 0; i < 16; ++i)
+            for (int e = 0; e < 4; ++e) pkt[4 * (4096 + q * 16 + i) + e] = tw2[2 * (i * 16 + 2 * q) + e];
+    }
+    SDSP_TRY(h->d_pkt.ensure(pkt.size() * 4), "alloc packed tables");
+    SDSP_TRY(hipMemcpyAsync(h->d_pkt.p, pkt.data(), pkt.size() * 4, hipMemcpyHostToDevice, h->stream),
+             "copy packed tables");
     // N = 1024 natural-order spectrum and twiddles for the wave-per-segment kernel (L - 1 <= 256)
     int hr1k = 0;
     if (L - 1 <= 256) {
@@ -215,6 +231,7 @@ int ols_build(sdsp_fir* h) {
     h->ols.packed = h->ols_packed;
     h->ols.segs_per_block = h->ols_segs;
     h->ols.xcd = h->ols_xcd;
+    h->ols.d_pkt = h->d_pkt.p;
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -325,6 +342,7 @@ void sdsp_fir_destroy(sdsp_fir* h) {
         h->d_tw2.release();
         h->d_H1k.release();
         h->d_tw1k.release();
+        h->d_pkt.release();
     }
     delete h;
 }
@@ -363,7 +381,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
         case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
         case SDSP_TUNE_OLS_SEGS_PER_BLOCK: h->ols_segs = value >= -1 ? value : 0; break;  // -1: XCD-local interleave
         case SDSP_TUNE_OLS_PACKED: h->ols_packed = (value >= 0 && value <= 6) ? value : 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 8) ? value : 0; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 9) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }

@@ -50,6 +50,7 @@ struct OlsPlan {
     int packed = 0;  // packed-FP32 interior kernel (kern_fir_ols_pk.hip): odd = asm table products, even = compiler-
                      // visible; 1-2 default scheduler, 3-4 max-ilp, 5-6 iterative-ilp
     int segs_per_block = 0;  // packed kernel: 0 persistent interleaved grid, > 0 consecutive segments per workgroup
+    void* d_pkt = nullptr;   // packed kernel tables, k-pair major (runtime.cpp ols_build)
     bool xcd = true;         // packed kernel, segs_per_block > 0: workgroup b % 8 (its XCD) takes a contiguous 1/8 of the chunks
 };
 constexpr int kOlsN = 4096;

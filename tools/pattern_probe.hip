@@ -254,6 +254,61 @@ void run_pchunk(const float2* x, float2* y, long long nsamp, int per, int lds, i
                 16.0 * nsamp / (ms * 1e-3) / 1e9);
 }
 
+// Persistent grid with a dynamic work queue per XCD: XCD b % 8 owns one contiguous
+// eighth of the segments; its workgroups take the next segment from an atomic counter
+// (the index for segment s + 1 is fetched while segment s moves), so the resident
+// workgroups of an XCD stay on one compact window, as a one-shot dispatch keeps them.
+__global__ void __launch_bounds__(256) dyn_k(const f4v* __restrict__ x, f4v* __restrict__ y, long long nseg,
+                                             unsigned long long* ctr) {
+    extern __shared__ float lds_dyn[];
+    __shared__ long long nxt_s[2];
+    const int t = threadIdx.x;
+    const int xc = blockIdx.x % 8;
+    const long long s8 = (nseg + 7) / 8;
+    const long long a = xc * s8;
+    const long long e = a + s8 < nseg ? a + s8 : nseg;
+    if (t == 0) nxt_s[0] = a + (long long)atomicAdd(ctr + xc, 1ULL);
+    __syncthreads();
+    long long s = nxt_s[0];
+    int par = 1;
+    while (s < e) {
+        if (t == 0) nxt_s[par] = a + (long long)atomicAdd(ctr + xc, 1ULL);
+        f4v q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = x[s * 2048 + t + 256 * i];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[s * 2048 + t + 256 * i] = q[i];
+        __syncthreads();
+        s = nxt_s[par];
+        par ^= 1;
+    }
+    if (nseg < 0) lds_dyn[t] = 0.f;
+}
+
+void run_dyn(const float2* x, float2* y, long long nsamp, int grid, int lds, int reps) {
+    const long long nseg = nsamp / 4096;
+    unsigned long long* ctr;
+    (void)hipMalloc(&ctr, 64);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    std::vector<float> ts;
+    for (int r = 0; r < reps + 1; ++r) {
+        (void)hipMemset(ctr, 0, 64);
+        (void)hipEventRecord(e0);
+        hipLaunchKernelGGL(dyn_k, dim3((unsigned)grid), dim3(256), lds, 0, (const f4v*)x, (f4v*)y, nseg, ctr);
+        (void)hipEventRecord(e1);
+        (void)hipEventSynchronize(e1);
+        float ms;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (r) ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    const float ms = ts[ts.size() / 2];
+    std::printf("DYN grid %5d lds %6d  %.3f ms  %.1f GB/s\n", grid, lds, ms, 16.0 * nsamp / (ms * 1e-3) / 1e9);
+    (void)hipFree(ctr);
+}
+
 int main() {
     const long long n = 1LL << 30;
     float2 *x, *y;
@@ -264,6 +319,15 @@ int main() {
 
     const int L = 70 * 1024;
     const int reps = 5;
+    if (getenv("PROBE_DYN")) {
+        run_dyn(x, y, n, 512, L, reps);
+        run_dyn(x, y, n, 1024, L, reps);
+        run_dyn(x, y, n, 512, 0, reps);
+        run_dyn(x, y, n, 2048, 0, reps);
+        run_lin<8, 0, 2>(x, y, n, L, reps);
+        run_pchunk<8>(x, y, n, 16, L, 0, reps);
+        return 0;
+    }
     if (getenv("PROBE_XCD")) {
         run_lin<2, 0, 0>(x, y, n, L, reps);
         run_lin<2, 0, 2>(x, y, n, L, reps);
