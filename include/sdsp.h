@@ -77,6 +77,8 @@ typedef enum {
     SDSP_E_IIR_INTERPOLATION_LESS_THAN_ONE = 16,
     /* SecondOrderErrorCode (src/filter/iir/sos.rs:19-21) */
     SDSP_E_SOS_COEFFICIENTS_NOT_IN_RANGE = 20,
+    /* NCOErrorCode (src/nco/mod.rs:7-10) */
+    SDSP_E_NCO_BANDWIDTH_OUT_OF_RANGE = 30,
     /* argument errors the reference reports by panicking */
     SDSP_E_INVALID_ARGUMENT = 90,
     SDSP_E_UNSUPPORTED = 91,
@@ -305,6 +307,69 @@ SDSP_API int sdsp_dot_execute(int dtype, const void* coefs, size_t len, int dire
 SDSP_API int sdsp_dot_execute_batched_device(int dtype, const void* coefs, size_t len, int direction,
                                              const void* d_samples, size_t n, size_t stride, size_t batch,
                                              void* d_out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * AutoCorrelator (src/filter/auto_correlator/mod.rs:26-214), SURVEY §8f row 3.
+ * precision: 0 = Complex<f32>, 1 = Complex<f64> (the reference's push() needs
+ * C = f64, :99-102; the f32 handle runs the same operations at f32).  After each
+ * push the output is sum_{j < window} x[n-j] * conj(x[n-j-delay]) over the delayed
+ * Window's unfilled tail (terms with j + delay >= window are zero), newest first,
+ * from zero — bit-identical to the reference order.  `channels` independent
+ * correlators, channel-major buffers.  Energy: sum of |x|^2 over the last
+ * window_size inputs (f64; the reference's running sum agrees to rounding).
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_acorr sdsp_acorr;
+/* AutoCorrelator::<C>::new(window_size, delay)        :51-62 */
+SDSP_API int sdsp_acorr_create(sdsp_acorr** out, size_t window_size, size_t delay, int precision, int device);
+SDSP_API void sdsp_acorr_destroy(sdsp_acorr* h);
+SDSP_API int sdsp_acorr_set_channels(sdsp_acorr* h, size_t channels);
+SDSP_API size_t sdsp_acorr_window_size(const sdsp_acorr* h);
+SDSP_API size_t sdsp_acorr_delay(const sdsp_acorr* h);
+/* reset  :76-85 */
+SDSP_API int sdsp_acorr_reset(sdsp_acorr* h);
+/* push (one sample, single channel)  :99-111;  write (push only)  :128-137 */
+SDSP_API int sdsp_acorr_push(sdsp_acorr* h, const void* sample);
+SDSP_API int sdsp_acorr_write(sdsp_acorr* h, const void* samples, size_t n);
+SDSP_API int sdsp_acorr_write_device(sdsp_acorr* h, const void* d_samples, size_t n, void* stream);
+/* execute() on the current windows (no push), one value per channel  :156-163 */
+SDSP_API int sdsp_acorr_execute(sdsp_acorr* h, void* out);
+/* execute_block: push then execute per sample  :181-191 */
+SDSP_API int sdsp_acorr_execute_block(sdsp_acorr* h, const void* in, size_t n, void* out);
+SDSP_API int sdsp_acorr_execute_block_device(sdsp_acorr* h, const void* d_in, size_t n, void* d_out, void* stream);
+/* get_energy, one f64 per channel  :212-214 */
+SDSP_API int sdsp_acorr_get_energy(sdsp_acorr* h, double* energy);
+SDSP_API int sdsp_acorr_synchronize(sdsp_acorr* h);
+
+/* ------------------------------------------------------------------------
+ * NCO (src/nco/mod.rs:27-187), SURVEY §8f row 4.  Phase and frequency are u32
+ * registers on the host (as in the reference); sample blocks are mixed on the
+ * device with the reference's 1024-entry f64 sine table and index rule.
+ * mix_block: out[i] = mix_up(x[i]) (down = 0) or mix_down(x[i]) (down = 1), then
+ * step() — the loop mix_up_block / mix_down_block spell out (:153-172; the
+ * reference's versions index an empty Vec and panic for any non-empty input).
+ * precision 0 = Complex<f32> samples (f32 table and product), 1 = Complex<f64>
+ * (bit-identical to the reference).
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_nco sdsp_nco;
+SDSP_API int sdsp_nco_create(sdsp_nco** out, int device);                     /* NCO::new  :36-50 */
+SDSP_API void sdsp_nco_destroy(sdsp_nco* h);
+SDSP_API int sdsp_nco_reset(sdsp_nco* h);                                     /* :53-56 */
+SDSP_API int sdsp_nco_set_frequency(sdsp_nco* h, double delta_theta);         /* :59-61 */
+SDSP_API int sdsp_nco_adjust_frequency(sdsp_nco* h, double dt);               /* :64-66 */
+SDSP_API double sdsp_nco_get_frequency(const sdsp_nco* h);                    /* :69-76 */
+SDSP_API int sdsp_nco_set_phase(sdsp_nco* h, double phi);                     /* :79-81 */
+SDSP_API int sdsp_nco_adjust_phase(sdsp_nco* h, double delta_phi);            /* :84-86 */
+SDSP_API double sdsp_nco_get_phase(const sdsp_nco* h);                        /* :89-91 */
+SDSP_API int sdsp_nco_step(sdsp_nco* h);                                      /* :94-96 */
+SDSP_API int sdsp_nco_sincos(const sdsp_nco* h, double* sin_cos);             /* :104-117 (sin, cos) */
+SDSP_API int sdsp_nco_set_internal_pll_bandwidth(sdsp_nco* h, double bw);     /* :124-132 */
+SDSP_API int sdsp_nco_pll_step(sdsp_nco* h, double delta_phi);                /* :135-138 */
+SDSP_API int sdsp_nco_get_state(const sdsp_nco* h, uint32_t* theta, uint32_t* delta_theta);
+SDSP_API int sdsp_nco_set_state(sdsp_nco* h, uint32_t theta, uint32_t delta_theta);
+SDSP_API int sdsp_nco_mix_block(sdsp_nco* h, int down, int precision, const void* in, size_t n, void* out);
+SDSP_API int sdsp_nco_mix_block_device(sdsp_nco* h, int down, int precision, const void* d_in, size_t n,
+                                       void* d_out, void* stream);
+SDSP_API int sdsp_nco_synchronize(sdsp_nco* h);
 
 /* ------------------------------------------------------------------------
  * Device utilities

@@ -12,6 +12,9 @@ from . import filter, group_delay, fft, dot_product, channelizer  # noqa: F401
 from .fft import FFT, FFTDirection, FFTFlags  # noqa: F401
 from .dot_product import DotProduct, Direction  # noqa: F401
 from .channelizer import Channelizer  # noqa: F401
+from . import nco  # noqa: F401
+from .nco import NCO, NCOError  # noqa: F401
+from .filter.auto_correlator import AutoCorrelator  # noqa: F401
 from .filter import (Filter, FIRFilter, DecimatingFIRFilter, PolyPhaseFilterBank,  # noqa: F401
                      InterpolatingFIRFilter, IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter,
                      InterpolatingIIRFilter)

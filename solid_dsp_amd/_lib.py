@@ -38,6 +38,7 @@ STATUS = {
     13: "SecondOrderSectionSizeMismatch", 14: "SecondOrderSectionSizeNotMultpleOf3",
     15: "DecimationLessThanOne", 16: "InterpolationLessThanOne",
     20: "CoefficientsNotInRange",
+    30: "BandwidthOutOfRange",
     90: "InvalidArgument", 91: "Unsupported",
     100: "DeviceError", 101: "NoDevice", 102: "OutOfMemory",
 }
@@ -178,6 +179,39 @@ def _optional_sigs():
         "sdsp_dot_execute_batched_device": (i, [i, vp, sz, i, vp, sz, sz, sz, vp, vp]),
         "sdsp_fft_len": (sz, [vp]),
         "sdsp_dot_execute": (i, [i, vp, sz, i, vp, sz, vp]),
+        # AutoCorrelator / NCO
+        "sdsp_acorr_create": (i, [vpp, sz, sz, i, i]),
+        "sdsp_acorr_destroy": (None, [vp]),
+        "sdsp_acorr_set_channels": (i, [vp, sz]),
+        "sdsp_acorr_window_size": (sz, [vp]),
+        "sdsp_acorr_delay": (sz, [vp]),
+        "sdsp_acorr_reset": (i, [vp]),
+        "sdsp_acorr_push": (i, [vp, vp]),
+        "sdsp_acorr_write": (i, [vp, vp, sz]),
+        "sdsp_acorr_write_device": (i, [vp, vp, sz, vp]),
+        "sdsp_acorr_execute": (i, [vp, vp]),
+        "sdsp_acorr_execute_block": (i, [vp, vp, sz, vp]),
+        "sdsp_acorr_execute_block_device": (i, [vp, vp, sz, vp, vp]),
+        "sdsp_acorr_get_energy": (i, [vp, dp]),
+        "sdsp_acorr_synchronize": (i, [vp]),
+        "sdsp_nco_create": (i, [vpp, i]),
+        "sdsp_nco_destroy": (None, [vp]),
+        "sdsp_nco_reset": (i, [vp]),
+        "sdsp_nco_set_frequency": (i, [vp, d]),
+        "sdsp_nco_adjust_frequency": (i, [vp, d]),
+        "sdsp_nco_get_frequency": (d, [vp]),
+        "sdsp_nco_set_phase": (i, [vp, d]),
+        "sdsp_nco_adjust_phase": (i, [vp, d]),
+        "sdsp_nco_get_phase": (d, [vp]),
+        "sdsp_nco_step": (i, [vp]),
+        "sdsp_nco_sincos": (i, [vp, dp]),
+        "sdsp_nco_set_internal_pll_bandwidth": (i, [vp, d]),
+        "sdsp_nco_pll_step": (i, [vp, d]),
+        "sdsp_nco_get_state": (i, [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "sdsp_nco_set_state": (i, [vp, C.c_uint32, C.c_uint32]),
+        "sdsp_nco_mix_block": (i, [vp, i, i, vp, sz, vp]),
+        "sdsp_nco_mix_block_device": (i, [vp, i, i, vp, sz, vp, vp]),
+        "sdsp_nco_synchronize": (i, [vp]),
     }
 
 

@@ -1,0 +1,415 @@
+// C-ABI runtime for the receive-chain objects next to the filter path
+// (SURVEY §8f rows 3-4): AutoCorrelator (src/filter/auto_correlator/mod.rs)
+// and NCO (src/nco/mod.rs).  The sample streams run in kern_rx.hip; the NCO's
+// scalar phase/frequency registers are host state, as in the reference.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "sdsp.h"
+#include "sdsp_host.hpp"
+#include "sdsp_kernels.hpp"
+
+using namespace sdsp;
+
+namespace {
+
+#define R_TRY(expr, what)                                      \
+    do {                                                       \
+        hipError_t _e = (expr);                                \
+        if (_e != hipSuccess) return device_status(_e, what);  \
+    } while (0)
+
+struct Guard {
+    int prev = -1;
+    explicit Guard(int d) {
+        (void)hipGetDevice(&prev);
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~Guard() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int check_gfx950(int device, int* cus) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) {
+        set_error("no HIP device visible (libsdsp has no CPU execution path)");
+        return SDSP_E_NO_DEVICE;
+    }
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess || std::strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+        set_error("libsdsp is built for gfx950");
+        return SDSP_E_NO_DEVICE;
+    }
+    if (cus) *cus = p.multiProcessorCount;
+    return SDSP_OK;
+}
+
+hipStream_t pick(void* user, hipStream_t own) { return user ? (hipStream_t)user : own; }
+size_t cbytes(int prec) { return prec == 0 ? 8 : 16; }
+int hist_dtype(int prec) { return prec == 0 ? SDSP_RC32 : SDSP_RC64; }  // sample size 8 / 16 bytes
+
+// constrain()  src/nco/mod.rs:175-187
+uint32_t constrain(double theta) {
+    const double d = theta / (2.0 * M_PI);
+    double f = d - std::trunc(d);  // f64::fract
+    if (f < 0.0) f += 1.0;
+    return (uint32_t)(f * (double)0xffffffffu);
+}
+
+}  // namespace
+
+// ===========================================================================
+// AutoCorrelator
+// ===========================================================================
+struct sdsp_acorr {
+    int prec = 1, device = 0;
+    size_t W = 0, d = 0, channels = 1;
+    DevBuf hist[2];  // [channels][W] oldest first
+    int cur = 0;
+    DevBuf energy;   // [channels] f64
+    DevBuf stage_in, stage_out;
+    hipStream_t stream = nullptr;
+    int K() const { return W > d ? (int)(W - d) : 0; }
+};
+
+namespace {
+int acorr_alloc(sdsp_acorr* h) {
+    const size_t hb = h->channels * h->W * cbytes(h->prec);
+    for (int i = 0; i < 2; ++i) {
+        R_TRY(h->hist[i].ensure(hb), "alloc history");
+        R_TRY(hipMemsetAsync(h->hist[i].p, 0, hb, h->stream), "zero history");
+    }
+    R_TRY(h->energy.ensure(h->channels * 8), "alloc energy");
+    R_TRY(hipMemsetAsync(h->energy.p, 0, h->channels * 8, h->stream), "zero energy");
+    h->cur = 0;
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int sdsp_acorr_create(sdsp_acorr** out, size_t window_size, size_t delay, int precision, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (window_size == 0 || (precision != 0 && precision != 1)) {
+        set_error("window_size must be > 0 (Window::new asserts capacity > 0); precision 0 = c32, 1 = c64");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    if (window_size > (1u << 30) || delay > (1u << 30)) {
+        set_error("window_size / delay too large");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    int st = check_gfx950(device, nullptr);
+    if (st) return st;
+    Guard g(device);
+    auto* h = new sdsp_acorr();
+    h->prec = precision;
+    h->device = device;
+    h->W = window_size;
+    h->d = delay;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        set_error("hipStreamCreate failed");
+        return SDSP_E_DEVICE;
+    }
+    st = acorr_alloc(h);
+    if (st) {
+        sdsp_acorr_destroy(h);
+        return st;
+    }
+    *out = h;
+    return SDSP_OK;
+}
+
+void sdsp_acorr_destroy(sdsp_acorr* h) {
+    if (!h) return;
+    {
+        Guard g(h->device);
+        if (h->stream) {
+            (void)hipStreamSynchronize(h->stream);
+            (void)hipStreamDestroy(h->stream);
+        }
+        h->hist[0].release();
+        h->hist[1].release();
+        h->energy.release();
+        h->stage_in.release();
+        h->stage_out.release();
+    }
+    delete h;
+}
+
+int sdsp_acorr_set_channels(sdsp_acorr* h, size_t channels) {
+    if (!h || channels == 0) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    h->channels = channels;
+    return acorr_alloc(h);
+}
+
+int sdsp_acorr_reset(sdsp_acorr* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    return acorr_alloc(h);
+}
+
+size_t sdsp_acorr_window_size(const sdsp_acorr* h) { return h ? h->W : 0; }
+size_t sdsp_acorr_delay(const sdsp_acorr* h) { return h ? h->d : 0; }
+
+// push n samples per channel; with d_out, the execute() value after every push
+static int acorr_run(sdsp_acorr* h, const void* d_in, size_t n, void* d_out, hipStream_t s) {
+    if (n == 0) return SDSP_OK;
+    const void* hist = h->hist[h->cur].p;
+    if (d_out)
+        R_TRY(launch_acorr(h->prec, d_in, hist, d_out, n, (int)h->W, (int)h->d, h->K(), h->channels, s), "acorr");
+    R_TRY(launch_acorr_energy(h->prec, d_in, hist, n, (int)h->W, (int)h->W, h->channels, (double*)h->energy.p, s),
+          "acorr energy");
+    R_TRY(launch_hist_update(hist_dtype(h->prec), d_in, hist, h->hist[h->cur ^ 1].p, n, (int)h->W, h->channels, s),
+          "history update");
+    h->cur ^= 1;
+    return SDSP_OK;
+}
+
+int sdsp_acorr_execute_block_device(sdsp_acorr* h, const void* d_in, size_t n, void* d_out, void* stream) {
+    if (!h || (n && (!d_in || !d_out))) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    return acorr_run(h, d_in, n, d_out, pick(stream, h->stream));
+}
+
+int sdsp_acorr_write_device(sdsp_acorr* h, const void* d_in, size_t n, void* stream) {
+    if (!h || (n && !d_in)) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    return acorr_run(h, d_in, n, nullptr, pick(stream, h->stream));
+}
+
+static int acorr_host(sdsp_acorr* h, const void* in, size_t n, void* out) {
+    if (!h || (n && !in)) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) return SDSP_OK;
+    Guard g(h->device);
+    const size_t bytes = h->channels * n * cbytes(h->prec);
+    R_TRY(h->stage_in.ensure(bytes), "stage in");
+    R_TRY(hipMemcpyAsync(h->stage_in.p, in, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    if (out) R_TRY(h->stage_out.ensure(bytes), "stage out");
+    int st = acorr_run(h, h->stage_in.p, n, out ? h->stage_out.p : nullptr, h->stream);
+    if (st) return st;
+    if (out) R_TRY(hipMemcpyAsync(out, h->stage_out.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_acorr_execute_block(sdsp_acorr* h, const void* in, size_t n, void* out) {
+    if (n && !out) return SDSP_E_INVALID_ARGUMENT;
+    return acorr_host(h, in, n, out);
+}
+
+int sdsp_acorr_write(sdsp_acorr* h, const void* in, size_t n) { return acorr_host(h, in, n, nullptr); }
+
+int sdsp_acorr_push(sdsp_acorr* h, const void* sample) {
+    if (!h || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
+    return acorr_host(h, sample, 1, nullptr);
+}
+
+int sdsp_acorr_execute(sdsp_acorr* h, void* out) {
+    if (!h || !out) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    const size_t bytes = h->channels * cbytes(h->prec);
+    R_TRY(h->stage_out.ensure(bytes), "stage out");
+    R_TRY(launch_acorr_current(h->prec, h->hist[h->cur].p, h->stage_out.p, (int)h->W, (int)h->d, h->K(), h->channels,
+                               h->stream),
+          "acorr execute");
+    R_TRY(hipMemcpyAsync(out, h->stage_out.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_acorr_get_energy(sdsp_acorr* h, double* energy) {
+    if (!h || !energy) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    R_TRY(hipMemcpyAsync(energy, h->energy.p, h->channels * 8, hipMemcpyDeviceToHost, h->stream), "D2H");
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_acorr_synchronize(sdsp_acorr* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// NCO
+// ===========================================================================
+struct sdsp_nco {
+    int device = 0, cus = 256;
+    uint32_t theta = 0, delta_theta = 0;
+    double alpha = 0.1, beta = 0.0;
+    double table[1024];
+    DevBuf d_table, stage_in, stage_out;
+    hipStream_t stream = nullptr;
+    size_t index() const { return (size_t)(((uint32_t)(theta + (1u << 21)) >> 22) & 0x3ffu); }  // :99-101
+};
+
+extern "C" {
+
+int sdsp_nco_create(sdsp_nco** out, int device) {  // NCO::new  src/nco/mod.rs:36-50
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    int cus = 256;
+    int st = check_gfx950(device, &cus);
+    if (st) return st;
+    Guard g(device);
+    auto* h = new sdsp_nco();
+    h->device = device;
+    h->cus = cus;
+    for (int i = 0; i < 1024; ++i) h->table[i] = std::sin(2.0 * M_PI * (double)i / 1024.0);
+    h->alpha = 0.1;
+    h->beta = std::sqrt(h->alpha);
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        set_error("hipStreamCreate failed");
+        return SDSP_E_DEVICE;
+    }
+    if (h->d_table.ensure(sizeof(h->table)) != hipSuccess ||
+        hipMemcpy(h->d_table.p, h->table, sizeof(h->table), hipMemcpyHostToDevice) != hipSuccess) {
+        sdsp_nco_destroy(h);
+        set_error("NCO table upload failed");
+        return SDSP_E_DEVICE;
+    }
+    *out = h;
+    return SDSP_OK;
+}
+
+void sdsp_nco_destroy(sdsp_nco* h) {
+    if (!h) return;
+    {
+        Guard g(h->device);
+        if (h->stream) {
+            (void)hipStreamSynchronize(h->stream);
+            (void)hipStreamDestroy(h->stream);
+        }
+        h->d_table.release();
+        h->stage_in.release();
+        h->stage_out.release();
+    }
+    delete h;
+}
+
+int sdsp_nco_reset(sdsp_nco* h) {  // :53-56
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->theta = 0;
+    h->delta_theta = 0;
+    return SDSP_OK;
+}
+int sdsp_nco_set_frequency(sdsp_nco* h, double dtheta) {  // :59-61
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->delta_theta = constrain(dtheta);
+    return SDSP_OK;
+}
+int sdsp_nco_adjust_frequency(sdsp_nco* h, double dt) {  // :64-66 (u32 add wraps in release builds)
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->delta_theta += constrain(dt);
+    return SDSP_OK;
+}
+// get_frequency (:69-76): (delta_theta as u64 / 2^32) is integer division, always 0 for a u32
+double sdsp_nco_get_frequency(const sdsp_nco* h) {
+    if (!h) return 0.0;
+    const double dt = (double)((uint64_t)h->delta_theta / (1ULL << 32)) * 2.0 * M_PI;
+    return dt > M_PI ? dt - 2.0 * M_PI : dt;
+}
+int sdsp_nco_set_phase(sdsp_nco* h, double phi) {  // :79-81
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->theta = constrain(phi);
+    return SDSP_OK;
+}
+int sdsp_nco_adjust_phase(sdsp_nco* h, double dphi) {  // :84-86
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->theta += constrain(dphi);
+    return SDSP_OK;
+}
+double sdsp_nco_get_phase(const sdsp_nco* h) {  // :89-91 (integer division as get_frequency)
+    return h ? (double)((uint64_t)h->theta / (1ULL << 32)) * 2.0 * M_PI : 0.0;
+}
+int sdsp_nco_step(sdsp_nco* h) {  // :94-96
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->theta += h->delta_theta;
+    return SDSP_OK;
+}
+int sdsp_nco_sincos(const sdsp_nco* h, double* sin_cos) {  // :104-117
+    if (!h || !sin_cos) return SDSP_E_INVALID_ARGUMENT;
+    sin_cos[0] = h->table[h->index()];
+    sin_cos[1] = h->table[(h->index() + 256) & 0x3ff];
+    return SDSP_OK;
+}
+int sdsp_nco_set_internal_pll_bandwidth(sdsp_nco* h, double bandwidth) {  // :124-132
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (bandwidth < 0.0) {
+        set_error("NCO Error Bandwidth out Range [0, inf)");
+        return SDSP_E_NCO_BANDWIDTH_OUT_OF_RANGE;
+    }
+    h->alpha = bandwidth;
+    h->beta = std::sqrt(bandwidth);
+    return SDSP_OK;
+}
+int sdsp_nco_pll_step(sdsp_nco* h, double delta_phi) {  // :135-138
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->delta_theta += constrain(delta_phi * h->alpha);
+    h->theta += constrain(delta_phi * h->beta);
+    return SDSP_OK;
+}
+int sdsp_nco_get_state(const sdsp_nco* h, uint32_t* theta, uint32_t* delta_theta) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (theta) *theta = h->theta;
+    if (delta_theta) *delta_theta = h->delta_theta;
+    return SDSP_OK;
+}
+int sdsp_nco_set_state(sdsp_nco* h, uint32_t theta, uint32_t delta_theta) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    h->theta = theta;
+    h->delta_theta = delta_theta;
+    return SDSP_OK;
+}
+
+// mix_up_block / mix_down_block (:153-172) as the per-sample loop they spell out:
+// out[i] = mix(x[i]) at theta, then step()
+int sdsp_nco_mix_block_device(sdsp_nco* h, int down, int precision, const void* d_in, size_t n, void* d_out,
+                              void* stream) {
+    if (!h || (precision != 0 && precision != 1) || (n && (!d_in || !d_out))) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    R_TRY(launch_nco_mix(precision, down != 0, d_in, d_out, n, (const double*)h->d_table.p, h->theta, h->delta_theta,
+                         h->cus, pick(stream, h->stream)),
+          "nco mix");
+    h->theta += (uint32_t)((uint64_t)n * h->delta_theta);  // n steps, wrapping
+    return SDSP_OK;
+}
+
+int sdsp_nco_mix_block(sdsp_nco* h, int down, int precision, const void* in, size_t n, void* out) {
+    if (!h || (precision != 0 && precision != 1) || (n && (!in || !out))) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) return SDSP_OK;
+    Guard g(h->device);
+    const size_t bytes = n * cbytes(precision);
+    R_TRY(h->stage_in.ensure(bytes), "stage in");
+    R_TRY(h->stage_out.ensure(bytes), "stage out");
+    R_TRY(hipMemcpyAsync(h->stage_in.p, in, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    int st = sdsp_nco_mix_block_device(h, down, precision, h->stage_in.p, n, h->stage_out.p, h->stream);
+    if (st) return st;
+    R_TRY(hipMemcpyAsync(out, h->stage_out.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_nco_synchronize(sdsp_nco* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+}  // extern "C"

@@ -141,6 +141,18 @@ struct DotArgs {
 };
 hipError_t launch_dot(int dtype, const DotArgs& a, hipStream_t s);
 
+// AutoCorrelator (kern_rx.hip); prec 0 = complex f32, 1 = complex f64.  hist: [channels][H]
+// oldest first (H = window size), K = max(W - delay, 0) product terms per output
+hipError_t launch_acorr(int prec, const void* x, const void* hist, void* y, size_t n, int H, int d, int K,
+                        size_t channels, hipStream_t s);
+hipError_t launch_acorr_current(int prec, const void* hist, void* out, int H, int d, int K, size_t channels,
+                                hipStream_t s);
+hipError_t launch_acorr_energy(int prec, const void* x, const void* hist, size_t n, int H, int W, size_t channels,
+                               double* energy, hipStream_t s);
+// NCO mix_up / mix_down over a block (kern_rx.hip): theta_i = theta0 + i dtheta (u32)
+hipError_t launch_nco_mix(int prec, bool down, const void* x, void* y, size_t n, const double* table, uint32_t theta0,
+                          uint32_t dtheta, int num_cus, hipStream_t s);
+
 hipError_t launch_bw_copy(const void* a, void* b, size_t bytes, int num_cus, hipStream_t s);
 hipError_t launch_synth_f32(float* out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,
                             hipStream_t s);

@@ -42,3 +42,6 @@ from .iir import (IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilt
 
 for _cls in (IIRFilter, DecimatingIIRFilter, InterpolatingIIRFilter):
     Filter.register(_cls)
+
+from . import auto_correlator  # noqa: E402,F401
+from .auto_correlator import AutoCorrelator  # noqa: E402,F401

@@ -85,6 +85,28 @@ def lib():
         "orc_fft_free": (None, [vp]),
         "orc_fft_method": (C.c_int, [vp]),
         "orc_channelize": (sz, [vp, sz, sz, vp, sz, vp]),
+        # sdsp_oracle_rx.cpp: AutoCorrelator / NCO
+        "orc_acorr_new": (vp, [sz, sz, C.c_int]),
+        "orc_acorr_free": (None, [vp]),
+        "orc_acorr_reset": (None, [vp]),
+        "orc_acorr_write": (None, [vp, vp, sz]),
+        "orc_acorr_execute_block": (None, [vp, vp, sz, vp]),
+        "orc_acorr_execute": (None, [vp, vp]),
+        "orc_acorr_get_energy": (C.c_double, [vp]),
+        "orc_nco_new": (vp, []),
+        "orc_nco_free": (None, [vp]),
+        "orc_nco_constrain": (C.c_uint32, [C.c_double]),
+        "orc_nco_set_frequency": (None, [vp, C.c_double]),
+        "orc_nco_adjust_frequency": (None, [vp, C.c_double]),
+        "orc_nco_set_phase": (None, [vp, C.c_double]),
+        "orc_nco_adjust_phase": (None, [vp, C.c_double]),
+        "orc_nco_reset": (None, [vp]),
+        "orc_nco_state": (None, [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "orc_nco_sincos": (None, [vp, dp]),
+        "orc_nco_set_pll_bandwidth": (C.c_int, [vp, C.c_double]),
+        "orc_nco_pll_step": (None, [vp, C.c_double]),
+        "orc_nco_step": (None, [vp]),
+        "orc_nco_mix_block": (None, [vp, C.c_int, dp, sz, dp]),
     }
     for name, (res, args) in list(sig.items()) + list(optional.items()):
         if not hasattr(L, name):
@@ -232,6 +254,75 @@ def active_lag(bw, zeta, k):
     if rc:
         raise ValueError(rc)
     return n, d
+
+
+class AutoCorr:
+    """Restated AutoCorrelator (oracle/sdsp_oracle_rx.cpp); dtype complex64 or complex128."""
+
+    def __init__(self, window_size, delay, dtype=np.complex128):
+        self.dt = np.dtype(dtype)
+        self.h = lib().orc_acorr_new(window_size, delay, 1 if self.dt == np.complex128 else 0)
+        if not self.h:
+            raise ValueError("window_size must be > 0")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_acorr_free(self.h)
+            self.h = None
+
+    def execute_block(self, x):
+        x = np.ascontiguousarray(x, dtype=self.dt)
+        out = np.zeros_like(x)
+        lib().orc_acorr_execute_block(self.h, _ptr(x), len(x), _ptr(out))
+        return out
+
+    def write(self, x):
+        x = np.ascontiguousarray(x, dtype=self.dt)
+        lib().orc_acorr_write(self.h, _ptr(x), len(x))
+
+    def execute(self):
+        out = np.zeros(1, dtype=self.dt)
+        lib().orc_acorr_execute(self.h, _ptr(out))
+        return out[0]
+
+    def get_energy(self):
+        return lib().orc_acorr_get_energy(self.h)
+
+    def reset(self):
+        lib().orc_acorr_reset(self.h)
+
+
+class Nco:
+    """Restated NCO (oracle/sdsp_oracle_rx.cpp)."""
+
+    def __init__(self):
+        self.h = lib().orc_nco_new()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_nco_free(self.h)
+            self.h = None
+
+    def __getattr__(self, name):
+        f = getattr(lib(), "orc_nco_" + name)
+        return lambda *a: f(self.h, *a)
+
+    def state(self):
+        th, dt = C.c_uint32(), C.c_uint32()
+        lib().orc_nco_state(self.h, C.byref(th), C.byref(dt))
+        return th.value, dt.value
+
+    def sincos(self):
+        sc = np.zeros(2)
+        lib().orc_nco_sincos(self.h, _dptr(sc))
+        return float(sc[0]), float(sc[1])
+
+    def mix_block(self, x, down=False):
+        x = np.ascontiguousarray(x, dtype=np.complex128)
+        out = np.zeros_like(x)
+        lib().orc_nco_mix_block(self.h, int(down), x.ctypes.data_as(C.POINTER(C.c_double)), len(x),
+                                out.ctypes.data_as(C.POINTER(C.c_double)))
+        return out
 
 
 def synth(seed, channel, start, count, complex_=False):
