@@ -265,13 +265,19 @@ SDSP_API int sdsp_iir_synchronize(sdsp_iir* h);
 /* ------------------------------------------------------------------------
  * FFT  (FFT::new / FFT::execute, src/fft/mod.rs:175-215).  direction: 0 FORWARD,
  * 1 REVERSE (unnormalised, like the reference).  precision: 0 = complex f32,
- * 1 = complex f64.  Power-of-two sizes up to 4096 run a radix-4 Stockham FFT in
- * LDS; other sizes a direct DFT.
+ * 1 = complex f64.  Sizes 1 .. 2^24, every size the reference plans (SURVEY §8f
+ * row 2).  Power-of-two sizes up to 4096 run a radix-4 Stockham FFT in LDS, larger
+ * powers of two a four-step FFT (two strided LDS passes, f64 inter-pass twiddles);
+ * other sizes up to 512 a direct DFT, larger ones Bluestein's chirp-z transform
+ * over a power-of-two convolution (where the reference plans Rader / mixed radix,
+ * src/fft/mod.rs:123-170; the results agree within the transforms' rounding).
  * ------------------------------------------------------------------------ */
 typedef struct sdsp_fft sdsp_fft;
 SDSP_API int sdsp_fft_create(sdsp_fft** out, size_t nfft, int direction, int precision, int device);
 SDSP_API void sdsp_fft_destroy(sdsp_fft* h);
 SDSP_API size_t sdsp_fft_len(const sdsp_fft* h);
+/* device plan: 0 direct DFT, 1 power of two in LDS, 2 Bluestein, 3 four-step power of two */
+SDSP_API int sdsp_fft_method(const sdsp_fft* h);
 /* `batch` contiguous transforms of nfft complex samples */
 SDSP_API int sdsp_fft_execute(sdsp_fft* h, const void* in, void* out, size_t batch);
 SDSP_API int sdsp_fft_execute_device(sdsp_fft* h, const void* d_in, void* d_out, size_t batch, void* stream);

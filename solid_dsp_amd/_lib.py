@@ -178,6 +178,7 @@ def _optional_sigs():
         "sdsp_fft_execute_device": (i, [vp, vp, vp, sz, vp]),
         "sdsp_dot_execute_batched_device": (i, [i, vp, sz, i, vp, sz, sz, sz, vp, vp]),
         "sdsp_fft_len": (sz, [vp]),
+        "sdsp_fft_method": (i, [vp]),
         "sdsp_dot_execute": (i, [i, vp, sz, i, vp, sz, vp]),
         # AutoCorrelator / NCO
         "sdsp_acorr_create": (i, [vpp, sz, sz, i, i]),

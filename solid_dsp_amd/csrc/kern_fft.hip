@@ -140,7 +140,121 @@ chan_kernel(const c2<T>* __restrict__ x, const c2<T>* __restrict__ hist, const T
     for (int c = threadIdx.x; c < M; c += blockDim.x) y[c] = r[c];
 }
 
+// Strided pass of the four-step FFT (power-of-two N = N1 N2 > 4096, both factors
+// <= 4096): transform t of L points reads element i at
+//   x[(t / G) S0 + (t % G) S1 + i Si]  and writes  y[(t / G) S0 + (t % G) T1 + i So],
+// times W_Ntw^{(t % G) i} when TW (the inter-pass twiddle, from f64 sincospi of
+// the exact phase (t % G) i mod Ntw).
+template <typename T, bool INV, bool TW>
+__global__ void __launch_bounds__(1024)
+fft_pass_kernel(const c2<T>* __restrict__ x, c2<T>* __restrict__ y, const c2<T>* __restrict__ tw, int L, int logL,
+                long long count, long long G, long long S0, long long S1, long long Si, long long T1, long long So,
+                long long Ntw, int nthr, int tpb) {
+    extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+    c2<T>* buf = reinterpret_cast<c2<T>*>(lds_raw);
+    const int sub = threadIdx.x / nthr, lane = threadIdx.x % nthr;
+    const long long t = (long long)blockIdx.x * tpb + sub;
+    c2<T>* a = buf + (size_t)sub * 2 * L;
+    c2<T>* b = a + L;
+    const long long g = t % G;
+    const long long ib = (t / G) * S0 + g * S1, ob = (t / G) * S0 + g * T1;
+    if (t < count)
+        for (int i = lane; i < L; i += nthr) a[i] = x[ib + i * Si];
+    __syncthreads();
+    c2<T>* r = stockham<T, INV>(a, b, L, logL, tw, lane, nthr);
+    if (t < count)
+        for (int i = lane; i < L; i += nthr) {
+            c2<T> v = r[i];
+            if constexpr (TW) {
+                const long long m = (g * (long long)i) % Ntw;
+                double sn, cs;
+                sincospi((INV ? 2.0 : -2.0) * (double)m / (double)Ntw, &sn, &cs);
+                v = cm(v, c2<T>{(T)cs, (T)sn});
+            }
+            y[ob + i * So] = v;
+        }
+}
+
+// Bluestein (chirp-z) steps for sizes that are not powers of two: w[n] = the
+// chirp of the transform direction, B = FFT_M(conj chirp, wrapped) / M
+template <typename T>
+__global__ void bluestein_in_kernel(const c2<T>* __restrict__ x, c2<T>* __restrict__ a, const c2<T>* __restrict__ w,
+                                    long long N, long long M, long long batch) {
+    const long long total = batch * M;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long b = i / M, m = i % M;
+        a[i] = m < N ? cm(x[b * N + m], w[m]) : c2<T>{T(0), T(0)};
+    }
+}
+template <typename T>
+__global__ void bluestein_mul_kernel(c2<T>* __restrict__ a, const c2<T>* __restrict__ B, long long M, long long batch) {
+    const long long total = batch * M;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x)
+        a[i] = cm(a[i], B[i % M]);
+}
+template <typename T>
+__global__ void bluestein_out_kernel(const c2<T>* __restrict__ a, c2<T>* __restrict__ y, const c2<T>* __restrict__ w,
+                                     long long N, long long M, long long batch) {
+    const long long total = batch * N;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const long long b = i / N, k = i % N;
+        y[i] = cm(a[b * M + k], w[k]);
+    }
+}
+
 // ---------------------------------------------------------------- launchers
+template <typename T>
+hipError_t launch_fft_pass_t(const FftPass& p, hipStream_t s) {
+    const int L = p.L;
+    const int nthr = L >= 4 ? L / 4 : 1;
+    const int tpb = nthr >= 256 ? 1 : 256 / nthr;
+    const size_t lds = (size_t)tpb * 2 * L * sizeof(c2<T>);
+    dim3 grid((unsigned)((p.count + tpb - 1) / tpb));
+#define SDSP_PASS(INV, TW)                                                                                       \
+    hipLaunchKernelGGL((fft_pass_kernel<T, INV, TW>), grid, dim3(nthr * tpb), lds, s, (const c2<T>*)p.x,          \
+                       (c2<T>*)p.y, (const c2<T>*)p.tw, L, p.logL, p.count, p.G, p.S0, p.S1, p.Si, p.T1, p.So, p.Ntw, \
+                       nthr, tpb)
+    if (p.inverse) {
+        if (p.Ntw) SDSP_PASS(true, true); else SDSP_PASS(true, false);
+    } else {
+        if (p.Ntw) SDSP_PASS(false, true); else SDSP_PASS(false, false);
+    }
+#undef SDSP_PASS
+    return hipGetLastError();
+}
+
+hipError_t launch_fft_pass(bool f64, const FftPass& p, hipStream_t s) {
+    if (p.count == 0) return hipSuccess;
+    return f64 ? launch_fft_pass_t<double>(p, s) : launch_fft_pass_t<float>(p, s);
+}
+
+hipError_t launch_bluestein(bool f64, int step, const void* in, void* out, const void* w_or_B, long long N, long long M,
+                            long long batch, hipStream_t s) {
+    const long long total = batch * (step == 2 ? N : M);
+    long long blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    dim3 grid((unsigned)blocks);
+#define SDSP_BLU(T)                                                                                               \
+    do {                                                                                                          \
+        if (step == 0)                                                                                            \
+            hipLaunchKernelGGL(bluestein_in_kernel<T>, grid, dim3(256), 0, s, (const c2<T>*)in, (c2<T>*)out,      \
+                               (const c2<T>*)w_or_B, N, M, batch);                                                \
+        else if (step == 1)                                                                                       \
+            hipLaunchKernelGGL(bluestein_mul_kernel<T>, grid, dim3(256), 0, s, (c2<T>*)out, (const c2<T>*)w_or_B, \
+                               M, batch);                                                                         \
+        else                                                                                                      \
+            hipLaunchKernelGGL(bluestein_out_kernel<T>, grid, dim3(256), 0, s, (const c2<T>*)in, (c2<T>*)out,     \
+                               (const c2<T>*)w_or_B, N, M, batch);                                                \
+    } while (0)
+    if (f64) SDSP_BLU(double);
+    else SDSP_BLU(float);
+#undef SDSP_BLU
+    return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_fft_t(const FftArgs& a, hipStream_t s) {
     const int N = a.N;

@@ -78,12 +78,97 @@ int make_twiddles(DevBuf& buf, size_t N, bool f64) {
 
 }  // namespace
 
+namespace {
+
+// power-of-two transform: Stockham in LDS (N <= 4096) or the four-step
+// decomposition N = N1 N2 (two strided passes, inter-pass twiddle) above
+struct Pow2Plan {
+    size_t N = 0;
+    int logN = 0, l1 = 0, l2 = 0;
+    DevBuf tw, tw1, tw2;
+    bool four_step() const { return N > 4096; }
+    int build(size_t n, bool f64) {
+        N = n;
+        logN = ilog2(n);
+        if (!four_step()) return make_twiddles(tw, N, f64);
+        l1 = logN / 2;
+        l2 = logN - l1;
+        int st = make_twiddles(tw1, (size_t)1 << l1, f64);
+        if (st) return st;
+        return make_twiddles(tw2, (size_t)1 << l2, f64);
+    }
+    // in -> out (may alias); tmp: batch * N samples when four_step()
+    hipError_t run(bool f64, const void* in, void* out, void* tmp, size_t batch, bool inverse, hipStream_t s) const {
+        if (!four_step()) {
+            FftArgs a{in, out, tw.p, (int)N, logN, true, inverse, batch};
+            return launch_fft(f64, a, s);
+        }
+        const long long n = (long long)N, N1 = 1LL << l1, N2 = 1LL << l2;
+        // pass 1: columns n2 (length N1, stride N2) -> tmp[k1][n2] * W_N^(n2 k1)
+        FftPass p1{in, tmp, tw1.p, (int)N1, l1, (long long)batch * N2, N2, n, 1, N2, 1, N2, n, inverse};
+        hipError_t e = launch_fft_pass(f64, p1, s);
+        if (e != hipSuccess) return e;
+        // pass 2: rows k1 (length N2) -> out[k1 + N1 k2]
+        FftPass p2{tmp, out, tw2.p, (int)N2, l2, (long long)batch * N1, N1, n, N2, 1, 1, N1, 0, inverse};
+        return launch_fft_pass(f64, p2, s);
+    }
+};
+
+// iterative radix-2 FFT in f64 on the host (Bluestein filter spectrum, plan time only)
+void host_fft_pow2(std::vector<double>& a, size_t M) {
+    for (size_t i = 1, j = 0; i < M; ++i) {
+        size_t bit = M >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            std::swap(a[2 * i], a[2 * j]);
+            std::swap(a[2 * i + 1], a[2 * j + 1]);
+        }
+    }
+    for (size_t len = 2; len <= M; len <<= 1) {
+        for (size_t k = 0; k < len / 2; ++k) {
+            const double ang = -2.0 * M_PI * (double)k / (double)len;
+            const double wr = std::cos(ang), wi = std::sin(ang);
+            for (size_t i = 0; i < M; i += len) {
+                double* u = &a[2 * (i + k)];
+                double* v = &a[2 * (i + k + len / 2)];
+                const double tr = v[0] * wr - v[1] * wi, ti = v[0] * wi + v[1] * wr;
+                v[0] = u[0] - tr;
+                v[1] = u[1] - ti;
+                u[0] += tr;
+                u[1] += ti;
+            }
+        }
+    }
+}
+
+int upload(DevBuf& buf, const std::vector<double>& v, bool f64) {
+    if (f64) {
+        F_TRY(buf.ensure(v.size() * 8), "alloc");
+        F_TRY(hipMemcpy(buf.p, v.data(), v.size() * 8, hipMemcpyHostToDevice), "upload");
+    } else {
+        std::vector<float> f(v.begin(), v.end());
+        F_TRY(buf.ensure(f.size() * 4), "alloc");
+        F_TRY(hipMemcpy(buf.p, f.data(), f.size() * 4, hipMemcpyHostToDevice), "upload");
+    }
+    return SDSP_OK;
+}
+
+constexpr size_t kDirectMax = 512;  // non-power-of-two sizes up to this run the direct DFT
+
+}  // namespace
+
 struct sdsp_fft {
     size_t N = 0;
     int direction = 0;  // 0 FORWARD, 1 REVERSE
     bool f64 = true;
     int device = 0;
+    int kind = 0;       // 0 direct DFT, 1 power of two, 2 Bluestein
     DevBuf tw, stage_in, stage_out;
+    Pow2Plan p2;        // kind 1: the transform; kind 2: the length-M convolution transform
+    size_t M = 0;       // Bluestein convolution length (power of two >= 2N - 1)
+    DevBuf chirp, spec; // Bluestein: w[N] of the direction, B[M] = FFT_M(conj chirp) / M
+    DevBuf work, tmp;   // device scratch, grown with the batch
     hipStream_t stream = nullptr;
 };
 
@@ -109,10 +194,6 @@ int sdsp_fft_create(sdsp_fft** out, size_t nfft, int direction, int precision, i
         return SDSP_E_INVALID_ARGUMENT;
     }
     if (direction != 0 && direction != 1) return SDSP_E_INVALID_ARGUMENT;
-    if (is_pow2(nfft) && nfft > 4096) {
-        set_error("power-of-two FFT sizes above 4096 are not supported on the device yet");
-        return SDSP_E_UNSUPPORTED;
-    }
     int st = check_gfx950(device);
     if (st) return st;
     Guard g(device);
@@ -123,7 +204,38 @@ int sdsp_fft_create(sdsp_fft** out, size_t nfft, int direction, int precision, i
     h->device = device;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete h; return device_status(e, "stream"); }
-    st = make_twiddles(h->tw, nfft, h->f64);
+    if (is_pow2(nfft)) {
+        h->kind = 1;
+        st = h->p2.build(nfft, h->f64);
+    } else if (nfft <= kDirectMax) {
+        h->kind = 0;
+        st = make_twiddles(h->tw, nfft, h->f64);
+    } else {
+        // Bluestein: X[k] = w[k] sum_n (x[n] w[n]) conj(w[k - n]),  w[n] = e^{-/+ j pi n^2 / N}
+        h->kind = 2;
+        size_t M = 1;
+        while (M < 2 * nfft - 1) M <<= 1;
+        h->M = M;
+        const double sgn = direction == 1 ? 1.0 : -1.0;
+        std::vector<double> w(2 * nfft), bb(2 * M, 0.0);
+        for (size_t n = 0; n < nfft; ++n) {
+            const unsigned long long q = (unsigned long long)((unsigned __int128)n * n % (2 * (unsigned __int128)nfft));
+            const double ang = sgn * M_PI * (double)q / (double)nfft;
+            w[2 * n] = std::cos(ang);
+            w[2 * n + 1] = std::sin(ang);
+            bb[2 * n] = w[2 * n];  // conj(w)
+            bb[2 * n + 1] = -w[2 * n + 1];
+            if (n) {
+                bb[2 * (M - n)] = w[2 * n];
+                bb[2 * (M - n) + 1] = -w[2 * n + 1];
+            }
+        }
+        host_fft_pow2(bb, M);
+        for (auto& v : bb) v /= (double)M;
+        st = upload(h->chirp, w, h->f64);
+        if (!st) st = upload(h->spec, bb, h->f64);
+        if (!st) st = h->p2.build(M, h->f64);
+    }
     if (st) { sdsp_fft_destroy(h); return st; }
     *out = h;
     return SDSP_OK;
@@ -137,6 +249,13 @@ void sdsp_fft_destroy(sdsp_fft* h) {
         h->tw.release();
         h->stage_in.release();
         h->stage_out.release();
+        h->p2.tw.release();
+        h->p2.tw1.release();
+        h->p2.tw2.release();
+        h->chirp.release();
+        h->spec.release();
+        h->work.release();
+        h->tmp.release();
     }
     delete h;
 }
@@ -146,14 +265,39 @@ size_t sdsp_fft_len(const sdsp_fft* h) { return h ? h->N : 0; }
 int sdsp_fft_execute_device(sdsp_fft* h, const void* d_in, void* d_out, size_t batch, void* stream) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (batch == 0) return SDSP_OK;
-    if (d_in == d_out && !is_pow2(h->N)) {
-        set_error("in-place direct DFT is not supported");
-        return SDSP_E_INVALID_ARGUMENT;
-    }
     Guard g(h->device);
-    FftArgs a{d_in, d_out, h->tw.p, (int)h->N, ilog2(h->N), is_pow2(h->N), h->direction == 1, batch};
-    F_TRY(launch_fft(h->f64, a, stream ? (hipStream_t)stream : h->stream), "fft");
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const size_t cb = h->f64 ? 16 : 8;
+    const bool inv = h->direction == 1;
+    if (h->kind == 0) {
+        if (d_in == d_out) {  // the direct DFT reads every input per output: work from a copy
+            F_TRY(h->work.ensure(batch * h->N * cb), "dft scratch");
+            F_TRY(hipMemcpyAsync(h->work.p, d_in, batch * h->N * cb, hipMemcpyDeviceToDevice, s), "dft copy");
+            d_in = h->work.p;
+        }
+        FftArgs a{d_in, d_out, h->tw.p, (int)h->N, ilog2(h->N), false, inv, batch};
+        F_TRY(launch_fft(h->f64, a, s), "fft");
+    } else if (h->kind == 1) {
+        if (h->p2.four_step()) F_TRY(h->tmp.ensure(batch * h->N * cb), "fft scratch");
+        F_TRY(h->p2.run(h->f64, d_in, d_out, h->tmp.p, batch, inv, s), "fft");
+    } else {
+        const long long N = (long long)h->N, M = (long long)h->M;
+        F_TRY(h->work.ensure(batch * h->M * cb), "bluestein scratch");
+        if (h->p2.four_step()) F_TRY(h->tmp.ensure(batch * h->M * cb), "bluestein scratch");
+        F_TRY(launch_bluestein(h->f64, 0, d_in, h->work.p, h->chirp.p, N, M, (long long)batch, s), "bluestein in");
+        F_TRY(h->p2.run(h->f64, h->work.p, h->work.p, h->tmp.p, batch, false, s), "bluestein fft");
+        F_TRY(launch_bluestein(h->f64, 1, nullptr, h->work.p, h->spec.p, N, M, (long long)batch, s), "bluestein mul");
+        F_TRY(h->p2.run(h->f64, h->work.p, h->work.p, h->tmp.p, batch, true, s), "bluestein ifft");
+        F_TRY(launch_bluestein(h->f64, 2, h->work.p, d_out, h->chirp.p, N, M, (long long)batch, s), "bluestein out");
+    }
     return SDSP_OK;
+}
+
+// plan kind (0 direct DFT, 1 power of two in LDS, 2 Bluestein, 3 four-step power of two)
+int sdsp_fft_method(const sdsp_fft* h) {
+    if (!h) return -1;
+    if (h->kind == 1 && h->p2.four_step()) return 3;
+    return h->kind;
 }
 
 // FFT::execute(&[Complex]) -> Vec<Complex> over `batch` contiguous transforms   src/fft/mod.rs:188-215

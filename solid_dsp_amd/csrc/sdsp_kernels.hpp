@@ -114,6 +114,19 @@ struct FftArgs {
     size_t batch;
 };
 hipError_t launch_fft(bool f64, const FftArgs& a, hipStream_t s);
+// strided pass of the four-step FFT (kern_fft.hip fft_pass_kernel); Ntw = 0: no inter-pass twiddle
+struct FftPass {
+    const void* x;
+    void* y;
+    const void* tw;  // [L] e^{-j 2 pi m / L}
+    int L, logL;
+    long long count, G, S0, S1, Si, T1, So, Ntw;
+    bool inverse;
+};
+hipError_t launch_fft_pass(bool f64, const FftPass& p, hipStream_t s);
+// Bluestein steps: 0 chirp in (x[N] -> a[M], zero padded), 1 a *= B, 2 chirp out (a -> y[N])
+hipError_t launch_bluestein(bool f64, int step, const void* in, void* out, const void* w_or_B, long long N, long long M,
+                            long long batch, hipStream_t s);
 
 // PFB + FFT channeliser (M power of two)
 struct ChanArgs {

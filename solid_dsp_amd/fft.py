@@ -1,8 +1,10 @@
 """``solid::fft`` on MI355X (src/fft/mod.rs:175-215).
 
 ``FFT(nfft, FFTDirection.FORWARD).execute(x)`` is ``FFT::new(nfft, FORWARD,
-ESTIMATE).execute(&x)``: unnormalised in both directions.  The device runs a
-radix-4 Stockham FFT (power-of-two sizes up to 4096) or a direct DFT.
+ESTIMATE).execute(&x)``: unnormalised in both directions, any size 1 .. 2^24.
+The device runs a radix-4 Stockham FFT in LDS (powers of two up to 4096), a
+four-step FFT (larger powers of two), a direct DFT (other sizes up to 512) or
+Bluestein's chirp-z transform (other sizes).
 """
 from __future__ import annotations
 
@@ -46,6 +48,13 @@ class FFT:
         if h is not None and h.value:
             L.lib().sdsp_fft_destroy(h)
             self._h = None
+
+    METHODS = {0: "direct DFT", 1: "Stockham (LDS)", 2: "Bluestein", 3: "four-step"}
+
+    @property
+    def method(self) -> str:
+        """Device plan of this size (the reference plans Rader / mixed radix / DFT leaves)."""
+        return self.METHODS[int(L.lib().sdsp_fft_method(self._h))]
 
     def execute(self, x) -> np.ndarray:
         """One transform of nfft samples, or a [batch, nfft] array of them."""

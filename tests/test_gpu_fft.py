@@ -35,6 +35,36 @@ def test_fft_vs_restatement(n, prec):
             assert rel_rms(y[b], ref) <= tol, (n, d, rel_rms(y[b], ref))
 
 
+@pytest.mark.parametrize("n,method", [(8192, "four-step"), (65536, "four-step"), (1 << 20, "four-step"),
+                                      (513, "Bluestein"), (1000, "Bluestein"), (500, "direct DFT"), (4097, "Bluestein"),
+                                      (10007, "Bluestein"), (3 * 5 * 7 * 11 * 13, "Bluestein"),
+                                      (100003, "Bluestein")])
+@pytest.mark.parametrize("prec", [np.complex64, np.complex128])
+def test_fft_large_and_any_size(n, method, prec):
+    """General sizes: four-step powers of two and Bluestein, both
+    directions, batched and in place, vs numpy (f64) and, up to 2^16, the restated
+    reference planner (whose DFT16 constants bound the f64 agreement near 1e-7)."""
+    import torch
+    rng = np.random.default_rng(n)
+    batch = 2 if n <= 1 << 16 else 1
+    x = (rng.standard_normal((batch, n)) + 1j * rng.standard_normal((batch, n))).astype(prec)
+    for d in (FFTDirection.FORWARD, FFTDirection.REVERSE):
+        f = FFT(n, d, precision=prec)
+        assert f.method == method
+        y = f.execute(x)
+        xs = x.astype(np.complex128)
+        ref = np.fft.fft(xs, axis=-1) if d == FFTDirection.FORWARD else np.fft.ifft(xs, axis=-1) * n
+        tol = 5e-6 if prec == np.complex64 else 1e-12
+        assert rel_rms(y, ref) <= tol, (n, d, rel_rms(y, ref))
+        if n <= 1 << 16:
+            assert rel_rms(y[0], offt(xs[0], int(d))) <= (5e-6 if prec == np.complex64 else 1e-7)
+        # device, in place
+        t = torch.from_numpy(x.copy()).to("cuda")
+        f.execute_device(t, t, batch, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        assert rel_rms(t.cpu().numpy(), y) <= (1e-6 if prec == np.complex64 else 1e-14)
+
+
 def test_fft_errors():
     with pytest.raises(sd.SdspError):
         FFT(0)
