@@ -586,7 +586,7 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
-        static const int kAbl[10] = {0, 1, 0, 0, 3, 3, 7, 8, 24, 40};  // 40: HBM only + spectrum table
+        static const int kAbl[11] = {0, 1, 0, 0, 3, 3, 7, 8, 24, 40, 16};  // 40: HBM only + spectrum table
         const int abl = kAbl[p.nomem];
         if (p.packed <= 2) return pk_default::launch_fir_ols_pk(p, x, y, n, channels, num_cus, s, lo, hi, abl);
         if (p.packed <= 4) return pk_ilp::launch_fir_ols_pk(p, x, y, n, channels, num_cus, s, lo, hi, abl);

@@ -564,7 +564,7 @@ hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n,
             case 8: SDSP_OLS_PK_D2V(8); break;
             case 24: SDSP_OLS_PK_D2V(24); break;
             case 40: SDSP_OLS_PK_D2V(40); break;
-            case 56: SDSP_OLS_PK_D2V(56); break;
+            case 16: SDSP_OLS_PK_D2V(16); break;
             default: return hipErrorInvalidValue;
         }
 #undef SDSP_OLS_PK_D2V

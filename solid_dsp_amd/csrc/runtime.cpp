@@ -381,7 +381,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
         case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
         case SDSP_TUNE_OLS_SEGS_PER_BLOCK: h->ols_segs = value >= -1 ? value : 0; break;  // -1: XCD-local interleave
         case SDSP_TUNE_OLS_PACKED: h->ols_packed = (value >= 0 && value <= 6) ? value : 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 9) ? value : 0; break;
+        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 10) ? value : 0; break;
         case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
         default: return SDSP_E_INVALID_ARGUMENT;
     }
