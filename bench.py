@@ -12,6 +12,10 @@ Other configs (BASELINE.json configs[2..4]):
   3  4-biquad cascade (scipy butter(8, 0.2) SOS), real f32, 1 GiS, block-parallel scan
   4  M=32 decimator, 256 taps (32 branches x 8), crcf, 1 GiS input per GPU
   5  1024-channel PFB + FFT channeliser, 8 streams x 2^24 samples per GPU
+SURVEY §8f rows (build-defined cases, same parity + measurement fields):
+  6  AutoCorrelator(64, 16), c32, 2^29 samples
+  7  NCO mix_down, c32, 2^30 samples
+  8  batched 2^20-point forward FFT (four-step), c32, 2^28 samples
 
 With N ranks each rank processes its own independent channel(s) (weak
 scaling, no collective in the timed region); RCCL is used afterwards only for
@@ -38,7 +42,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5])
+    p.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5, 6, 7, 8])
     p.add_argument("--log2n", type=int, default=30, help="samples per GPU per step (configs 2-4)")
     p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"], help="config 2 kernel")
     p.add_argument("--cpu-samples", type=int, default=None,
@@ -374,9 +378,154 @@ class Cfg1FIR:
                          "sequential dot)", samples, CPU_CHUNK)
 
 
-WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan}
+class Cfg6ACorr:
+    """AutoCorrelator(window 64, delay 16), Complex<f32>, 2^29 samples: one read of x and
+    one write of y per sample (src/filter/auto_correlator/mod.rs:181-191)."""
+    metric = "Msamples/sec AutoCorrelator(64, 16) execute_block, c32; % HBM roofline"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        self.W, self.D = 64, 16
+        self.n = 1 << min(args.log2n, 29)
+        self.f = sd.AutoCorrelator(self.W, self.D, dtype=np.complex64, device=dev)
+        self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        self.d_out = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        self.bytes_per_step = 16 * self.n
+        self.dtype = "c32 (complex-f32 products and sums, f64 energy)"
+        self.kernel = "acorr_kernel<float> (LDS-staged conj products, 256 outputs per workgroup) + energy + history"
+        self.parity_check = "bit mismatches vs the c32 restatement over the first 2^20 outputs (must be 0)"
+        self.workload = f"cfg6: AutoCorrelator(64, 16), c32, 2^{int(np.log2(self.n))} samples per channel"
+        self.algo_name = "acorr"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng):
+        import oracle_lib as O
+        import torch
+        import solid_dsp_amd as sd
+        m = 1 << 20
+        g = sd.AutoCorrelator(self.W, self.D, dtype=np.complex64)
+        g.execute_block_device(self.d_in, m, self.d_out, stream)
+        torch.cuda.synchronize()
+        x = self.d_in[:m].cpu().numpy()
+        y = self.d_out[:m].cpu().numpy()
+        ref = O.AutoCorr(self.W, self.D, np.complex64).execute_block(x)
+        return float(np.count_nonzero(y.view(np.uint64) != ref.view(np.uint64)))
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        chunk = CPU_CHUNK // 4
+        x = O.synth(SEED, 0, 0, chunk, complex_=True).astype(np.complex128)
+        f = O.AutoCorr(self.W, self.D, np.complex128)
+        return timed_cpu(lambda c: f.execute_block(x), "AutoCorrelator<f64> restatement (two Windows, memmove push, "
+                         "to_vec + zip sum per sample)", samples, chunk)
+
+
+class Cfg7NCO:
+    """NCO mix_down of a Complex<f32> stream, frequency 2 pi 0.0123 (src/nco/mod.rs:147-172)."""
+    metric = "Msamples/sec NCO mix_down, c32; % HBM roofline"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        self.n = 1 << args.log2n
+        self.freq = 2 * np.pi * 0.0123
+        self.f = sd.NCO(device=dev)
+        self.f.set_frequency(self.freq)
+        self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        self.d_out = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        self.bytes_per_step = 16 * self.n
+        self.dtype = "c32 (f32 copy of the f64 sine table, complex-f32 product)"
+        self.kernel = "nco_mix_kernel<float, true> (u32 phase per sample, LDS sine table)"
+        self.parity_check = "rel_rms vs the f64 restatement over the first 2^20 outputs (tolerance 1e-6)"
+        self.workload = f"cfg7: NCO mix_down, dtheta = constrain(2 pi 0.0123), c32, 2^{args.log2n} samples"
+        self.algo_name = "nco"
+
+    def step(self, stream):
+        self.f.mix_block_device(self.d_in, self.n, self.d_out, down=True, precision=0, stream=stream)
+
+    def parity(self, stream, rng):
+        import oracle_lib as O
+        import torch
+        import solid_dsp_amd as sd
+        m = 1 << 20
+        g = sd.NCO()
+        g.set_frequency(self.freq)
+        g.mix_block_device(self.d_in, m, self.d_out, down=True, precision=0, stream=stream)
+        torch.cuda.synchronize()
+        x = self.d_in[:m].cpu().numpy().astype(np.complex128)
+        y = self.d_out[:m].cpu().numpy()
+        o = O.Nco()
+        o.set_frequency(self.freq)
+        ref = o.mix_block(x, True)
+        return float(np.linalg.norm(y - ref) / np.linalg.norm(ref))
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = O.synth(SEED, 0, 0, CPU_CHUNK, complex_=True).astype(np.complex128)
+        o = O.Nco()
+        o.set_frequency(self.freq)
+        return timed_cpu(lambda c: o.mix_block(x, True), "NCO restatement (table lookup + mix_down + step per "
+                         "sample, f64)", samples, CPU_CHUNK)
+
+
+class Cfg8FFT:
+    """Batched 2^20-point forward FFT, Complex<f32>, 256 transforms per step (src/fft/mod.rs)."""
+    metric = "Msamples/sec batched 2^20-point FFT, c32; % HBM roofline"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import FFT, FFTDirection
+        self.N = 1 << 20
+        self.n = 1 << min(args.log2n, 28)
+        self.batch = self.n // self.N
+        self.f = FFT(self.N, FFTDirection.FORWARD, precision=np.complex64, device=dev)
+        self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        self.d_out = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        # algorithmic bytes: one read and one write of every sample; the four-step
+        # plan makes two passes, so its floor is 2x this (DESIGN.md)
+        self.bytes_per_step = 16 * self.n
+        self.dtype = "c32 (complex-f32 butterflies, f64-derived twiddles)"
+        self.kernel = f"fft_pass_kernel<float> x2 (four-step 1024 x 1024, {self.f.method})"
+        self.parity_check = "rel_rms of transform 0 vs numpy f64 (tolerance 5e-6)"
+        self.workload = f"cfg8: {self.batch} x 2^20-point forward FFT, c32, out of place"
+        self.algo_name = "fft"
+
+    def step(self, stream):
+        self.f.execute_device(self.d_in, self.d_out, self.batch, stream)
+
+    def parity(self, stream, rng):
+        import torch
+        self.step(stream)
+        torch.cuda.synchronize()
+        x = self.d_in[: self.N].cpu().numpy().astype(np.complex128)
+        y = self.d_out[: self.N].cpu().numpy()
+        ref = np.fft.fft(x)
+        return float(np.linalg.norm(y - ref) / np.linalg.norm(ref))
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        L = O.lib()
+        h = L.orc_fft_new(self.N, 0)
+        x = O.synth(SEED, 0, 0, self.N, complex_=True).astype(np.complex128)
+        y = np.zeros(self.N, np.complex128)
+        try:
+            return timed_cpu(lambda c: L.orc_fft_execute(h, O._ptr(x), O._ptr(y)),
+                             "FFT restatement (reference mixed-radix planner, f64), one 2^20 transform per call",
+                             samples, self.N)
+        finally:
+            L.orc_fft_free(h)
+
+
+WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT}
 # bounded CPU samples: about 10-20 s of single-thread work each on a current x86 host
-CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32}
+CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 << 25, 7: 1 << 28, 8: 1 << 24}
 CPU_CHUNK = 1 << 22
 
 
