@@ -79,6 +79,12 @@ typedef enum {
     SDSP_E_SOS_COEFFICIENTS_NOT_IN_RANGE = 20,
     /* NCOErrorCode (src/nco/mod.rs:7-10) */
     SDSP_E_NCO_BANDWIDTH_OUT_OF_RANGE = 30,
+    /* AGCErrorCode (src/auto_gain_control/mod.rs:49-56) */
+    SDSP_E_AGC_BANDWIDTH_OUT_OF_RANGE = 40,
+    SDSP_E_AGC_SIGNAL_LEVEL_OUT_OF_RANGE = 41,
+    SDSP_E_AGC_GAIN_BELOW_THRESHOLD = 42,
+    SDSP_E_AGC_SCALE_BELOW_THRESHOLD = 43,
+    SDSP_E_AGC_SAMPLES_TOO_LOW = 44,
     /* argument errors the reference reports by panicking */
     SDSP_E_INVALID_ARGUMENT = 90,
     SDSP_E_UNSUPPORTED = 91,
@@ -376,6 +382,59 @@ SDSP_API int sdsp_nco_mix_block(sdsp_nco* h, int down, int precision, const void
 SDSP_API int sdsp_nco_mix_block_device(sdsp_nco* h, int down, int precision, const void* d_in, size_t n,
                                        void* d_out, void* stream);
 SDSP_API int sdsp_nco_synchronize(sdsp_nco* h);
+
+/* ------------------------------------------------------------------------
+ * AGC (src/auto_gain_control/mod.rs:97-677), SURVEY §8f row 4.  A handle is a
+ * bank of `channels` independent AGCs (channel-major sample buffers) with
+ * device-resident state; one lane per channel runs the reference's per-sample
+ * recurrence (execute :214-246) in f64, with the squelch state machine
+ * (update_squelch_mode :631-677).  Samples are f64 (sample_type 0) or
+ * Complex<f64> (1), the two types the reference's trait bounds admit.  The
+ * recurrence calls exp/ln/log10 per sample: results agree with the reference to
+ * libm rounding (the device's f64 exp/log are not glibc's), not bit for bit.
+ * Setters apply to every channel; sdsp_agc_get_state reads one channel.
+ * ------------------------------------------------------------------------ */
+typedef struct sdsp_agc sdsp_agc;
+typedef enum {  /* SquelchMode  :84-94 */
+    SDSP_SQUELCH_UNKNOWN = 0,
+    SDSP_SQUELCH_ENABLED = 1,
+    SDSP_SQUELCH_RISE = 2,
+    SDSP_SQUELCH_SIGNALHI = 3,
+    SDSP_SQUELCH_FALL = 4,
+    SDSP_SQUELCH_SIGNALLO = 5, /* the reference's SINGALLO */
+    SDSP_SQUELCH_TIMEOUT = 6,
+    SDSP_SQUELCH_DISABLED = 7
+} sdsp_squelch_mode;
+typedef struct {  /* struct AGC  :96-108 */
+    double gain, scale, bandwidth, alpha, energy_estimate;
+    int32_t lock, squelch_mode;
+    double squelch_threshold;
+    uint64_t squelch_timeout, squelch_timer;
+} sdsp_agc_state;
+SDSP_API int sdsp_agc_create(sdsp_agc** out, size_t channels, int device);      /* AGC::new  :136-149 */
+SDSP_API void sdsp_agc_destroy(sdsp_agc* h);
+SDSP_API size_t sdsp_agc_channels(const sdsp_agc* h);
+SDSP_API int sdsp_agc_reset(sdsp_agc* h);                                       /* :178-188 */
+/* execute_block  :273-285 (execute per sample :214-246); n samples per channel */
+SDSP_API int sdsp_agc_execute_block(sdsp_agc* h, int sample_type, const void* in, size_t n, void* out);
+SDSP_API int sdsp_agc_execute_block_device(sdsp_agc* h, int sample_type, const void* d_in, size_t n, void* d_out,
+                                           void* stream);
+/* init  :568-586 — per channel: gain = 1 / (sqrt(mean |x|^2) + 1e-16); levels[c] receives the level */
+SDSP_API int sdsp_agc_init(sdsp_agc* h, int sample_type, const void* in, size_t n, double* levels);
+SDSP_API int sdsp_agc_lock(sdsp_agc* h);                                        /* :303-305 */
+SDSP_API int sdsp_agc_unlock(sdsp_agc* h);                                      /* :322-324 */
+SDSP_API int sdsp_agc_set_bandwidth(sdsp_agc* h, double bandwidth);             /* :374-386 */
+SDSP_API int sdsp_agc_set_signal_level(sdsp_agc* h, double level);              /* :416-428 */
+SDSP_API int sdsp_agc_set_rssi(sdsp_agc* h, double rssi);                       /* :458-466 */
+SDSP_API int sdsp_agc_set_gain(sdsp_agc* h, double gain);                       /* :497-504 */
+SDSP_API int sdsp_agc_set_scale(sdsp_agc* h, double scale);                     /* :535-542 */
+SDSP_API int sdsp_agc_squelch_enable(sdsp_agc* h);                              /* :589-591 */
+SDSP_API int sdsp_agc_squelch_disable(sdsp_agc* h);                             /* :594-596 */
+SDSP_API int sdsp_agc_squelch_set_threshold(sdsp_agc* h, double threshold);     /* :612-614 */
+SDSP_API int sdsp_agc_squelch_set_timeout(sdsp_agc* h, uint64_t timeout);       /* :622-624 */
+SDSP_API int sdsp_agc_get_state(sdsp_agc* h, size_t channel, sdsp_agc_state* st);
+SDSP_API int sdsp_agc_set_state(sdsp_agc* h, size_t channel, const sdsp_agc_state* st);
+SDSP_API int sdsp_agc_synchronize(sdsp_agc* h);
 
 /* ------------------------------------------------------------------------
  * Device utilities

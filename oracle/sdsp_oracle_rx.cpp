@@ -1,6 +1,6 @@
 // ============================================================================
 // sdsp_oracle_rx.cpp — CPU RESTATEMENT of the receive-chain objects next to the
-// filter path: AutoCorrelator and NCO.
+// filter path: AutoCorrelator, NCO and AGC.
 // TEST INFRASTRUCTURE ONLY (see sdsp_oracle.cpp's header): loaded by tests/ and
 // bench.py's cpu_baseline leg, never by the product library.
 //
@@ -19,6 +19,9 @@
 //     mix_up_block / mix_down_block (:153-172) index a Vec of length 0 and panic
 //     for any non-empty input; the block restatement here is the per-sample
 //     composition `mix_up(x); step()` those functions spell out.
+//   * AGC  src/auto_gain_control/mod.rs:97-677 for f64 and Complex<f64> samples:
+//     execute (:214-246), update_squelch_mode (:631-677; the usize timer wraps as
+//     in a release build), init (:568-586) and the setters, with libm's exp/ln/log10.
 // Compiled with -ffp-contract=off (no FMA, as rustc).
 // ============================================================================
 #include <cmath>
@@ -102,6 +105,70 @@ struct NCO {
     void step() { theta += delta_theta; }  // wrapping_add  :94-96
     cpx<double> mix_up(cpx<double> x) const { return cmul(cpx<double>{cos_(), sin_()}, x); }  // :141-144
     cpx<double> mix_down(cpx<double> x) const { return cmul(conj(cpx<double>{cos_(), sin_()}), x); }  // :147-150
+};
+
+// AGC  src/auto_gain_control/mod.rs:84-677.  T = f64 or Complex<f64> (the trait
+// bounds Real<Output = f64> + Mul<f64> admit only these two).
+enum Squelch { UNKNOWN, ENABLED, RISE, SIGNALHI, FALL, SINGALLO, TIMEOUT, DISABLED };  // :85-94
+struct AGC {
+    double gain = 1.0, scale = 1.0, bandwidth = 0.1, alpha = 0.1, energy_estimate = 1.0;  // new  :136-149
+    bool lock = false;
+    int squelch_mode = DISABLED;
+    double squelch_threshold = 0.0;
+    uint64_t squelch_timeout = 100, squelch_timer = 0;
+
+    void reset() {  // :178-188
+        gain = 1.0;
+        energy_estimate = 1.0;
+        lock = false;
+        squelch_mode = squelch_mode == DISABLED ? DISABLED : ENABLED;
+    }
+    double get_rssi() const { return std::log10(gain) * -20.0; }  // :442-444
+    void update_squelch_mode() {  // :631-677
+        const bool exceeded = get_rssi() > squelch_threshold;
+        switch (squelch_mode) {
+            case ENABLED: squelch_mode = exceeded ? RISE : ENABLED; break;
+            case RISE: squelch_mode = exceeded ? SIGNALHI : FALL; break;
+            case SIGNALHI: squelch_mode = exceeded ? SIGNALHI : FALL; break;
+            case FALL:
+                squelch_timer = squelch_timeout;
+                squelch_mode = exceeded ? SIGNALHI : SINGALLO;
+                break;
+            case SINGALLO:
+                squelch_timer -= 1;  // usize; wraps as a release build does (debug panics at 0)
+                squelch_mode = squelch_timer == 0 ? TIMEOUT : exceeded ? SIGNALHI : SINGALLO;
+                break;
+            case TIMEOUT: squelch_mode = ENABLED; break;
+            default: squelch_mode = DISABLED;
+        }
+    }
+    // execute  :214-246 for an unlocked AGC, after `out` and its energy: the
+    // energy update, the gain update and the squelch; true when the squelch hands
+    // back the input (mode ENABLED)
+    bool update(double ee) {
+        energy_estimate = (1.0 - alpha) * energy_estimate + ee * alpha;
+        if (energy_estimate > 0.000001) gain *= std::exp(-0.5 * alpha * std::log(energy_estimate));
+        if (gain > 1000000.0) gain = 1000000.0;
+        update_squelch_mode();
+        return squelch_mode == ENABLED;
+    }
+    double execute(double x) {
+        const double out = x * gain;
+        if (lock) {
+            energy_estimate = (1.0 - alpha) * energy_estimate + out * out * alpha;
+            return out;
+        }
+        return update(out * out) ? x : out * scale;  // (out.conj() * out).real() for f64
+    }
+    cpx<double> execute(cpx<double> x) {
+        const cpx<double> out{x.re * gain, x.im * gain};
+        const double ee = cmul(conj(out), out).re;
+        if (lock) {
+            energy_estimate = (1.0 - alpha) * energy_estimate + ee * alpha;
+            return out;
+        }
+        return update(ee) ? x : cpx<double>{out.re * scale, out.im * scale};
+    }
 };
 
 }  // namespace orx
@@ -201,5 +268,63 @@ void orc_nco_mix_block(void* h, int down, const double* x, size_t n, double* out
         p->step();
     }
 }
+
+// ---- AGC: sample_type 0 = f64, 1 = Complex<f64> -------------------------------
+void* orc_agc_new() { return new AGC(); }
+void orc_agc_free(void* h) { delete (AGC*)h; }
+void orc_agc_reset(void* h) { ((AGC*)h)->reset(); }
+void orc_agc_execute_block(void* h, int sample_type, const double* x, size_t n, double* out) {  // :273-285
+    auto* a = (AGC*)h;
+    for (size_t i = 0; i < n; ++i) {
+        if (sample_type == 1) {
+            const cpx<double> r = a->execute(cpx<double>{x[2 * i], x[2 * i + 1]});
+            out[2 * i] = r.re;
+            out[2 * i + 1] = r.im;
+        } else {
+            out[i] = a->execute(x[i]);
+        }
+    }
+}
+int orc_agc_init(void* h, int sample_type, const double* x, size_t n, double* level) {  // :568-586
+    if (n == 0) return 44;
+    double x2 = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+        if (sample_type == 1) {
+            const cpx<double> v{x[2 * i], x[2 * i + 1]};
+            x2 += cmul(v, conj(v)).re;
+        } else {
+            x2 += x[i] * x[i];
+        }
+    }
+    x2 = std::sqrt(x2 / (double)n) + 1e-16;
+    *level = x2;
+    if (x2 <= 0.0) return 41;
+    ((AGC*)h)->gain = 1.0 / x2;  // set_signal_level  :416-428
+    ((AGC*)h)->energy_estimate = 1.0;
+    return 0;
+}
+int orc_agc_set_bandwidth(void* h, double bw) {  // :374-386
+    if (!(bw >= 0.0 && bw <= 1.0)) return 40;
+    ((AGC*)h)->bandwidth = bw;
+    ((AGC*)h)->alpha = bw;
+    return 0;
+}
+void orc_agc_set_rssi(void* h, double rssi) {  // :458-466
+    auto* a = (AGC*)h;
+    a->gain = std::pow(10.0, -rssi / 20.0);
+    if (a->gain < 1e-16) a->gain = 1e-16;
+    a->energy_estimate = 1.0;
+}
+void orc_agc_set_gain(void* h, double g) { ((AGC*)h)->gain = g; }
+void orc_agc_set_scale(void* h, double s) { ((AGC*)h)->scale = s; }
+void orc_agc_lock(void* h, int on) { ((AGC*)h)->lock = on != 0; }
+void orc_agc_squelch(void* h, int enable) { ((AGC*)h)->squelch_mode = enable ? ENABLED : DISABLED; }
+void orc_agc_squelch_set_threshold(void* h, double t) { ((AGC*)h)->squelch_threshold = t; }
+void orc_agc_squelch_set_timeout(void* h, uint64_t t) { ((AGC*)h)->squelch_timeout = t; }
+double orc_agc_get_gain(void* h) { return ((AGC*)h)->gain; }
+double orc_agc_get_energy(void* h) { return ((AGC*)h)->energy_estimate; }
+double orc_agc_get_rssi(void* h) { return ((AGC*)h)->get_rssi(); }
+int orc_agc_get_mode(void* h) { return ((AGC*)h)->squelch_mode; }
+uint64_t orc_agc_get_timer(void* h) { return ((AGC*)h)->squelch_timer; }
 
 }  // extern "C"

@@ -14,6 +14,8 @@ from .dot_product import DotProduct, Direction  # noqa: F401
 from .channelizer import Channelizer  # noqa: F401
 from . import nco  # noqa: F401
 from .nco import NCO, NCOError  # noqa: F401
+from . import auto_gain_control  # noqa: F401
+from .auto_gain_control import AGC, AGCError, AGCErrorCode, SquelchMode  # noqa: F401
 from .filter.auto_correlator import AutoCorrelator  # noqa: F401
 from .filter import (Filter, FIRFilter, DecimatingFIRFilter, PolyPhaseFilterBank,  # noqa: F401
                      InterpolatingFIRFilter, IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter,

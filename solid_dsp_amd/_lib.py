@@ -39,6 +39,8 @@ STATUS = {
     15: "DecimationLessThanOne", 16: "InterpolationLessThanOne",
     20: "CoefficientsNotInRange",
     30: "BandwidthOutOfRange",
+    40: "BandwidthOutOfRange", 41: "SignalLevelOutOfRange", 42: "GainBelowThreshold", 43: "ScaleBelowThreshold",
+    44: "SamplesTooLow",
     90: "InvalidArgument", 91: "Unsupported",
     100: "DeviceError", 101: "NoDevice", 102: "OutOfMemory",
 }
@@ -213,7 +215,35 @@ def _optional_sigs():
         "sdsp_nco_mix_block": (i, [vp, i, i, vp, sz, vp]),
         "sdsp_nco_mix_block_device": (i, [vp, i, i, vp, sz, vp, vp]),
         "sdsp_nco_synchronize": (i, [vp]),
+        "sdsp_agc_create": (i, [vpp, sz, i]),
+        "sdsp_agc_destroy": (None, [vp]),
+        "sdsp_agc_channels": (sz, [vp]),
+        "sdsp_agc_reset": (i, [vp]),
+        "sdsp_agc_execute_block": (i, [vp, i, vp, sz, vp]),
+        "sdsp_agc_execute_block_device": (i, [vp, i, vp, sz, vp, vp]),
+        "sdsp_agc_init": (i, [vp, i, vp, sz, dp]),
+        "sdsp_agc_lock": (i, [vp]),
+        "sdsp_agc_unlock": (i, [vp]),
+        "sdsp_agc_set_bandwidth": (i, [vp, d]),
+        "sdsp_agc_set_signal_level": (i, [vp, d]),
+        "sdsp_agc_set_rssi": (i, [vp, d]),
+        "sdsp_agc_set_gain": (i, [vp, d]),
+        "sdsp_agc_set_scale": (i, [vp, d]),
+        "sdsp_agc_squelch_enable": (i, [vp]),
+        "sdsp_agc_squelch_disable": (i, [vp]),
+        "sdsp_agc_squelch_set_threshold": (i, [vp, d]),
+        "sdsp_agc_squelch_set_timeout": (i, [vp, C.c_uint64]),
+        "sdsp_agc_get_state": (i, [vp, sz, C.POINTER(AgcState)]),
+        "sdsp_agc_set_state": (i, [vp, sz, C.POINTER(AgcState)]),
+        "sdsp_agc_synchronize": (i, [vp]),
     }
+
+
+class AgcState(C.Structure):
+    """sdsp_agc_state (include/sdsp.h) = the fields of struct AGC (src/auto_gain_control/mod.rs:96-108)."""
+    _fields_ = [("gain", C.c_double), ("scale", C.c_double), ("bandwidth", C.c_double), ("alpha", C.c_double),
+                ("energy_estimate", C.c_double), ("lock", C.c_int32), ("squelch_mode", C.c_int32),
+                ("squelch_threshold", C.c_double), ("squelch_timeout", C.c_uint64), ("squelch_timer", C.c_uint64)]
 
 
 def lib():

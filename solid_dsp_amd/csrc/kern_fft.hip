@@ -13,6 +13,8 @@
 //   X[m]   = FFT_M(v[m])
 // one workgroup per (frame, stream); the branch dot products write v straight
 // into the LDS buffer the FFT runs in.
+#include <cstdlib>
+
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 
@@ -144,7 +146,11 @@ chan_kernel(const c2<T>* __restrict__ x, const c2<T>* __restrict__ hist, const T
 // <= 4096): transform t of L points reads element i at
 //   x[(t / G) S0 + (t % G) S1 + i Si]  and writes  y[(t / G) S0 + (t % G) T1 + i So],
 // times W_Ntw^{(t % G) i} when TW (the inter-pass twiddle, from f64 sincospi of
-// the exact phase (t % G) i mod Ntw).
+// the exact phase (t % G) i mod Ntw).  A workgroup runs `tpb` consecutive
+// transforms (tpb divides G): when their elements interleave with unit stride
+// (S1 == 1 or T1 == 1) the group loads / stores them with consecutive lanes on
+// consecutive transforms, so every wave touches 8 * tpb-byte runs instead of one
+// 8-byte element per row.
 template <typename T, bool INV, bool TW>
 __global__ void __launch_bounds__(1024)
 fft_pass_kernel(const c2<T>* __restrict__ x, c2<T>* __restrict__ y, const c2<T>* __restrict__ tw, int L, int logL,
@@ -153,26 +159,48 @@ fft_pass_kernel(const c2<T>* __restrict__ x, c2<T>* __restrict__ y, const c2<T>*
     extern __shared__ __attribute__((aligned(16))) char lds_raw[];
     c2<T>* buf = reinterpret_cast<c2<T>*>(lds_raw);
     const int sub = threadIdx.x / nthr, lane = threadIdx.x % nthr;
-    const long long t = (long long)blockIdx.x * tpb + sub;
-    c2<T>* a = buf + (size_t)sub * 2 * L;
-    c2<T>* b = a + L;
-    const long long g = t % G;
-    const long long ib = (t / G) * S0 + g * S1, ob = (t / G) * S0 + g * T1;
-    if (t < count)
-        for (int i = lane; i < L; i += nthr) a[i] = x[ib + i * Si];
-    __syncthreads();
-    c2<T>* r = stockham<T, INV>(a, b, L, logL, tw, lane, nthr);
-    if (t < count)
-        for (int i = lane; i < L; i += nthr) {
-            c2<T> v = r[i];
-            if constexpr (TW) {
-                const long long m = (g * (long long)i) % Ntw;
-                double sn, cs;
-                sincospi((INV ? 2.0 : -2.0) * (double)m / (double)Ntw, &sn, &cs);
-                v = cm(v, c2<T>{(T)cs, (T)sn});
-            }
-            y[ob + i * So] = v;
+    const int nth = blockDim.x, tot = tpb * L;
+    const int ltpb = __builtin_ctz(tpb);  // tpb and L are powers of two
+    const long long t0 = (long long)blockIdx.x * tpb;
+    const long long g0 = t0 % G;
+    const long long ib = (t0 / G) * S0 + g0 * S1, ob = (t0 / G) * S0 + g0 * T1;
+    const int ntr = count - t0 < tpb ? (int)(count - t0) : tpb;
+    if (S1 == 1) {
+        for (int e = threadIdx.x; e < tot; e += nth) {
+            const int c = e & (tpb - 1), i = e >> ltpb;
+            if (c < ntr) buf[(size_t)c * 2 * L + i] = x[ib + c + i * Si];
         }
+    } else {
+        for (int e = threadIdx.x; e < tot; e += nth) {
+            const int i = e & (L - 1), c = e >> logL;
+            if (c < ntr) buf[(size_t)c * 2 * L + i] = x[ib + c * S1 + i * Si];
+        }
+    }
+    __syncthreads();
+    c2<T>* a = buf + (size_t)sub * 2 * L;
+    c2<T>* r = stockham<T, INV>(a, a + L, L, logL, tw, lane, nthr);
+    const int roff = (int)(r - a);  // 0 or L, the same for every transform of the group
+    auto out = [&](int c, int i) {
+        c2<T> v = buf[(size_t)c * 2 * L + roff + i];
+        if constexpr (TW) {
+            const long long m = ((g0 + c) * (long long)i) & (Ntw - 1);  // Ntw = N, a power of two
+            double sn, cs;
+            sincospi((INV ? 2.0 : -2.0) * (double)m / (double)Ntw, &sn, &cs);
+            v = cm(v, c2<T>{(T)cs, (T)sn});
+        }
+        y[ob + c * T1 + i * So] = v;
+    };
+    if (T1 == 1) {
+        for (int e = threadIdx.x; e < tot; e += nth) {
+            const int c = e & (tpb - 1), i = e >> ltpb;
+            if (c < ntr) out(c, i);
+        }
+    } else {
+        for (int e = threadIdx.x; e < tot; e += nth) {
+            const int i = e & (L - 1), c = e >> logL;
+            if (c < ntr) out(c, i);
+        }
+    }
 }
 
 // Bluestein (chirp-z) steps for sizes that are not powers of two: w[n] = the
@@ -209,9 +237,20 @@ __global__ void bluestein_out_kernel(const c2<T>* __restrict__ a, c2<T>* __restr
 template <typename T>
 hipError_t launch_fft_pass_t(const FftPass& p, hipStream_t s) {
     const int L = p.L;
-    const int nthr = L >= 4 ? L / 4 : 1;
-    const int tpb = nthr >= 256 ? 1 : 256 / nthr;
-    const size_t lds = (size_t)tpb * 2 * L * sizeof(c2<T>);
+    // transforms per workgroup: up to kMaxGroup interleaved transforms in <= kLdsCap
+    // bytes of LDS (two L-point buffers each), dividing G; <= 1024 threads
+    static const int kMaxGroup = [] {
+        const char* e = std::getenv("SDSP_FFT_GROUP");
+        const int v = e ? std::atoi(e) : 4;
+        return v >= 1 && v <= 64 ? v : 4;
+    }();
+    constexpr size_t kLdsCap = 128 * 1024;
+    const size_t per = 2 * (size_t)L * sizeof(c2<T>);
+    int tpb = 1;
+    while (tpb * 2 <= kMaxGroup && (size_t)tpb * 2 * per <= kLdsCap && p.G % (tpb * 2) == 0) tpb *= 2;
+    int nthr = L >= 4 ? L / 4 : 1;
+    while (nthr * tpb > 1024) nthr /= 2;
+    const size_t lds = (size_t)tpb * per;
     dim3 grid((unsigned)((p.count + tpb - 1) / tpb));
 #define SDSP_PASS(INV, TW)                                                                                       \
     hipLaunchKernelGGL((fft_pass_kernel<T, INV, TW>), grid, dim3(nthr * tpb), lds, s, (const c2<T>*)p.x,          \

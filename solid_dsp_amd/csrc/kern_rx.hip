@@ -10,7 +10,7 @@
 // With K = max(W - d, 0) the sum is
 //     y[n] = (((0 + p[n]) + p[n-1]) + ...) + p[n-K+1],   p[m] = x[m] * conj(x[m-d]),
 // the zero-product terms j >= K leave the sum unchanged (it starts at +0 and is
-// never -0).  Each workgroup owns 256 consecutive outputs; p over the window the
+// never -0).  Each workgroup owns 2048 consecutive outputs (8 per lane); p over the window the
 // outputs need is built once in LDS (one num-complex product per input, the
 // reference's rounding) and every lane adds its K terms newest first, in chunks
 // of kChunk so W is unbounded.  Bit-identical to the restatement at the handle's
@@ -24,6 +24,13 @@
 // (table[(idx + 256) & 1023], table[idx]), idx = ((theta + 2^21) >> 22) & 1023
 // (:99-121) from the handle's 1024-entry f64 sine table, staged in LDS;
 // mix_up = phasor * x, mix_down = conj(phasor) * x (num-complex Mul).
+//
+// AGC (src/auto_gain_control/mod.rs:214-246, :631-677).  A serial non-linear
+// recurrence per channel (gain depends on every earlier sample through exp/ln),
+// so one lane runs one channel; a 64-lane workgroup serves 64 channels and
+// stages kAgcS samples of each through LDS so that HBM sees 16 * kAgcS-byte
+// runs per channel instead of one sample per lane per row.
+#include "sdsp.h"
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 
@@ -31,10 +38,23 @@ namespace sdsp {
 
 namespace {
 
-constexpr int kTile = 256;    // outputs per workgroup
-constexpr int kChunk = 1024;  // j-terms staged per pass
+constexpr int kTile = 256;           // lanes per workgroup
+constexpr int kR = 8;                // consecutive outputs per lane
+constexpr int kOut = kTile * kR;     // outputs per workgroup
+constexpr int kChunk = 1024;         // j-terms staged per pass
+// one spare slot per 8: lane t reads slot 8t + o, i.e. LDS element 9t + ..., so the
+// 32 (c32) or 16 (c64) lanes of one LDS cycle hit distinct banks
+__host__ __device__ constexpr int pad8(int s) { return s + (s >> 3); }
 
 template <typename T> __device__ inline cpx<T> conj_(cpx<T> a) { return {a.re, -a.im}; }
+
+// Workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 share one);
+// remap so each XCD streams its own contiguous eighth of the buffer — the
+// one-shot order that ran at copy speed in tools/pattern_probe.hip (ORD 2).
+__device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned nb) {
+    const unsigned q = nb / 8;
+    return b < 8 * q ? (b % 8) * q + b / 8 : b;
+}
 
 template <typename T>
 __device__ inline cpx<T> ext_at(const cpx<T>* __restrict__ x, const cpx<T>* __restrict__ hist, long long j, int H) {
@@ -43,35 +63,88 @@ __device__ inline cpx<T> ext_at(const cpx<T>* __restrict__ x, const cpx<T>* __re
     return zero_v<cpx<T>>();
 }
 
+// Lane t owns outputs o_r = n0 + kR t + r (r < kR).  Within a chunk of terms
+// [j0, j0 + cj), output o_r adds p[o_r - j0 - jj] for jj = 0, 1, ... newest first;
+// p[n0 + kR t + q - j0] (q = r - jj) is shared by all r, so the lane walks q
+// downward, reads each p once from LDS and adds it to every accumulator whose
+// jj = r - q lies in [0, cj) — the same additions in the same order as the
+// one-output-per-lane form, with kR-fold fewer LDS reads.
 template <typename T>
 __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__ x, const cpx<T>* __restrict__ hist,
                                                       cpx<T>* __restrict__ y, long long n, int H, int d, int K) {
-    __shared__ cpx<T> p[kTile + kChunk - 1];
+    __shared__ cpx<T> p[pad8(kOut + kChunk - 1) + 1];
     const int ch = blockIdx.y;
     x += (long long)ch * n;
     y += (long long)ch * n;
     hist += (long long)ch * H;
     const int t = threadIdx.x;
-    const long long n0 = (long long)blockIdx.x * kTile;
-    const long long me = n0 + t;
-    cpx<T> acc = zero_v<cpx<T>>();
+    const long long n0 = (long long)xcd_order(blockIdx.x, gridDim.x) * kOut;
+    cpx<T> acc[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) acc[r] = zero_v<cpx<T>>();
     for (int j0 = 0; j0 < K; j0 += kChunk) {
         const int cj = K - j0 < kChunk ? K - j0 : kChunk;
-        // p[m] for m in [n0 - j0 - cj + 1, n0 + kTile - 1 - j0]: slot s <-> m = base + s
+        // p[m] for m in [n0 - j0 - cj + 1, n0 + kOut - 1 - j0]: slot s <-> m = base + s
         const long long base = n0 - j0 - cj + 1;
-        const int cnt = kTile + cj - 1;
+        const int cnt = kOut + cj - 1;
         __syncthreads();  // previous chunk's readers are done
-        for (int s = t; s < cnt; s += kTile) {
-            const long long m = base + s;
-            p[s] = mul_(ext_at(x, hist, m, H), conj_(ext_at(x, hist, m - d, H)));
+        // every load of the chunk is issued before the first product: the loads of
+        // one lane are independent, so the wave keeps kLd x 2 requests in flight
+        constexpr int kLd = (kOut + kChunk - 1 + kTile - 1) / kTile;
+        cpx<T> va[kLd], vb[kLd];
+        if (base - d >= 0 && base + cnt <= n) {  // interior tile: plain loads
+#pragma unroll
+            for (int k = 0; k < kLd; ++k) {
+                const int s = t + k * kTile;
+                if (s < cnt) {
+                    va[k] = x[base + s];
+                    vb[k] = x[base + s - d];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kLd; ++k) {
+                const int s = t + k * kTile;
+                if (s < cnt) {
+                    va[k] = ext_at(x, hist, base + s, H);
+                    vb[k] = ext_at(x, hist, base + s - d, H);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kLd; ++k) {
+            const int s = t + k * kTile;
+            if (s < cnt) p[pad8(s)] = mul_(va[k], conj_(vb[k]));
         }
         __syncthreads();
-        // output me adds p[me - j] for j = j0 .. j0 + cj - 1, newest first (slot t + cj - 1 - j)
-        const int s0 = t + cj - 1;
+        // slot of p[n0 + kR t + q - j0] is kR t + q + cj - 1
+        const int s0 = kR * t + cj - 1;
+        auto edge = [&](int q) {
+            const cpx<T> v = p[pad8(s0 + q)];
+#pragma unroll
+            for (int r = 0; r < kR; ++r)
+                if (r - q >= 0 && r - q < cj) acc[r] = add_(acc[r], v);
+        };
+        if (cj >= kR) {
+            for (int q = kR - 1; q >= 0; --q) edge(q);           // head: r >= q
 #pragma unroll 4
-        for (int j = 0; j < cj; ++j) acc = add_(acc, p[s0 - j]);
+            for (int q = -1; q > kR - 1 - cj; --q) {              // body: every r
+                const cpx<T> v = p[pad8(s0 + q)];
+#pragma unroll
+                for (int r = 0; r < kR; ++r) acc[r] = add_(acc[r], v);
+            }
+            for (int q = kR - 1 - cj; q > -cj; --q) edge(q);     // tail: r - q < cj
+        } else {
+            for (int q = kR - 1; q > -cj; --q) edge(q);
+        }
     }
-    if (me < n) y[me] = acc;
+    // stage through LDS for coalesced stores
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kR; ++r) p[pad8(kR * t + r)] = acc[r];
+    __syncthreads();
+    for (int s = t; s < kOut; s += kTile)
+        if (n0 + s < n) y[n0 + s] = p[pad8(s)];
 }
 
 // execute() on the current window (no push): the output for the newest history sample
@@ -111,19 +184,150 @@ __global__ void __launch_bounds__(256) acorr_energy_kernel(const cpx<T>* __restr
 }
 
 template <typename T, bool DOWN>
+__device__ __forceinline__ cpx<T> nco_one(const T* lut, cpx<T> v, long long i, uint32_t theta0, uint32_t dtheta) {
+    const uint32_t th = theta0 + (uint32_t)i * dtheta;  // wrapping u32: theta_0 + i dtheta mod 2^32
+    const uint32_t idx = ((th + (1u << 21)) >> 22) & 0x3ffu;
+    cpx<T> ph = {lut[(idx + 256) & 0x3ffu], lut[idx]};
+    if constexpr (DOWN) ph = conj_(ph);
+    return mul_(ph, v);
+}
+
+// One-shot, XCD-ordered: a workgroup mixes kU x 256 consecutive V-sample vectors
+// (32 KB of c32 input), issuing all its loads before staging the f32/f64 copy of
+// the sine table in LDS.
+constexpr int kNcoU = 8;
+template <typename T, bool DOWN, int V>
 __global__ void __launch_bounds__(256) nco_mix_kernel(const cpx<T>* __restrict__ x, cpx<T>* __restrict__ y, long long n,
                                                       const double* __restrict__ table, uint32_t theta0,
                                                       uint32_t dtheta) {
+    struct alignas(V * sizeof(cpx<T>)) Vec { cpx<T> s[V]; };
     __shared__ T lut[1024];
+    const long long nv = n / V;
+    const Vec* xv = reinterpret_cast<const Vec*>(x);
+    Vec* yv = reinterpret_cast<Vec*>(y);
+    const long long base = (long long)xcd_order(blockIdx.x, gridDim.x) * 256 * kNcoU + threadIdx.x;
+    Vec r[kNcoU];
+#pragma unroll
+    for (int u = 0; u < kNcoU; ++u)
+        if (base + 256 * u < nv) r[u] = xv[base + 256 * u];
     for (int i = threadIdx.x; i < 1024; i += 256) lut[i] = (T)table[i];
     __syncthreads();
-    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-        const uint32_t th = theta0 + (uint32_t)i * dtheta;  // wrapping u32: theta_0 + i dtheta mod 2^32
-        const uint32_t idx = ((th + (1u << 21)) >> 22) & 0x3ffu;
-        cpx<T> ph = {lut[(idx + 256) & 0x3ffu], lut[idx]};
-        if constexpr (DOWN) ph = conj_(ph);
-        y[i] = mul_(ph, x[i]);
+#pragma unroll
+    for (int u = 0; u < kNcoU; ++u) {
+        const long long v = base + 256 * u;
+        if (v < nv) {
+#pragma unroll
+            for (int k = 0; k < V; ++k) r[u].s[k] = nco_one<T, DOWN>(lut, r[u].s[k], v * V + k, theta0, dtheta);
+            yv[v] = r[u];
+        }
     }
+    if (blockIdx.x == 0 && threadIdx.x < n - nv * V) {  // ragged tail (c32, odd n)
+        const long long i = nv * V + threadIdx.x;
+        y[i] = nco_one<T, DOWN>(lut, x[i], i, theta0, dtheta);
+    }
+}
+
+// ---------------------------------------------------------------- AGC
+constexpr int kAgcS = 16;  // samples per channel per LDS chunk
+
+template <bool CPLX> struct AgcSample;
+template <> struct AgcSample<false> {
+    double v;
+    __device__ double energy() const { return v * v; }  // (out.conj() * out).real() for f64
+    __device__ AgcSample scaled(double g) const { return {v * g}; }
+};
+template <> struct AgcSample<true> {
+    double re, im;
+    // (conj(out) * out).re = re * re - (-im) * im  (num-complex Mul, no FMA)
+    __device__ double energy() const { return re * re - (-im) * im; }
+    __device__ AgcSample scaled(double g) const { return {re * g, im * g}; }
+};
+
+// update_squelch_mode  :631-677 (usize timer wraps, as a release build does)
+__device__ __forceinline__ void agc_squelch(sdsp_agc_state& s) {
+    if (s.squelch_mode == SDSP_SQUELCH_DISABLED || s.squelch_mode == SDSP_SQUELCH_UNKNOWN) {
+        s.squelch_mode = SDSP_SQUELCH_DISABLED;  // `_ => DISABLED`; the rssi it computes is unused
+        return;
+    }
+    const bool exceeded = log10(s.gain) * -20.0 > s.squelch_threshold;  // get_rssi  :442-444
+    switch (s.squelch_mode) {
+        case SDSP_SQUELCH_ENABLED: s.squelch_mode = exceeded ? SDSP_SQUELCH_RISE : SDSP_SQUELCH_ENABLED; break;
+        case SDSP_SQUELCH_RISE: s.squelch_mode = exceeded ? SDSP_SQUELCH_SIGNALHI : SDSP_SQUELCH_FALL; break;
+        case SDSP_SQUELCH_SIGNALHI: s.squelch_mode = exceeded ? SDSP_SQUELCH_SIGNALHI : SDSP_SQUELCH_FALL; break;
+        case SDSP_SQUELCH_FALL:
+            s.squelch_timer = s.squelch_timeout;
+            s.squelch_mode = exceeded ? SDSP_SQUELCH_SIGNALHI : SDSP_SQUELCH_SIGNALLO;
+            break;
+        case SDSP_SQUELCH_SIGNALLO:
+            s.squelch_timer -= 1;
+            s.squelch_mode = s.squelch_timer == 0 ? SDSP_SQUELCH_TIMEOUT
+                             : exceeded            ? SDSP_SQUELCH_SIGNALHI
+                                                   : SDSP_SQUELCH_SIGNALLO;
+            break;
+        default: s.squelch_mode = SDSP_SQUELCH_ENABLED;  // TIMEOUT
+    }
+}
+
+// execute  :214-246
+template <bool CPLX>
+__device__ __forceinline__ AgcSample<CPLX> agc_execute(sdsp_agc_state& s, AgcSample<CPLX> in) {
+    const AgcSample<CPLX> out = in.scaled(s.gain);
+    s.energy_estimate = (1.0 - s.alpha) * s.energy_estimate + out.energy() * s.alpha;
+    if (s.lock) return out;
+    if (s.energy_estimate > 0.000001) s.gain *= exp(-0.5 * s.alpha * log(s.energy_estimate));
+    if (s.gain > 1000000.0) s.gain = 1000000.0;
+    agc_squelch(s);
+    if (s.squelch_mode == SDSP_SQUELCH_ENABLED) return in;
+    return out.scaled(s.scale);
+}
+
+template <bool CPLX>
+__global__ void __launch_bounds__(64) agc_kernel(const AgcSample<CPLX>* __restrict__ x, AgcSample<CPLX>* __restrict__ y,
+                                                 long long n, sdsp_agc_state* __restrict__ state, long long channels) {
+    __shared__ AgcSample<CPLX> buf[64 * (kAgcS + 1)];  // row per channel, one spare slot
+    const int t = threadIdx.x;
+    const long long ch0 = (long long)blockIdx.x * 64;
+    const long long me = ch0 + t;
+    sdsp_agc_state s;
+    if (me < channels) s = state[me];
+    for (long long i0 = 0; i0 < n; i0 += kAgcS) {
+        const int cnt = n - i0 < kAgcS ? (int)(n - i0) : kAgcS;
+#pragma unroll
+        for (int k = 0; k < kAgcS; ++k) {  // lane e of a row group reads consecutive samples of one channel
+            const int e = t + 64 * k, c = e / kAgcS, j = e % kAgcS;
+            if (j < cnt && ch0 + c < channels) buf[c * (kAgcS + 1) + j] = x[(ch0 + c) * n + i0 + j];
+        }
+        __syncthreads();
+        if (me < channels)
+            for (int j = 0; j < cnt; ++j) {
+                AgcSample<CPLX>& v = buf[t * (kAgcS + 1) + j];
+                v = agc_execute<CPLX>(s, v);
+            }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kAgcS; ++k) {
+            const int e = t + 64 * k, c = e / kAgcS, j = e % kAgcS;
+            if (j < cnt && ch0 + c < channels) y[(ch0 + c) * n + i0 + j] = buf[c * (kAgcS + 1) + j];
+        }
+        __syncthreads();
+    }
+    if (me < channels) state[me] = s;
+}
+
+// init  :568-586 then set_signal_level  :416-428
+template <bool CPLX>
+__global__ void __launch_bounds__(64) agc_init_kernel(const AgcSample<CPLX>* __restrict__ x, long long n,
+                                                      sdsp_agc_state* __restrict__ state, double* __restrict__ levels,
+                                                      long long channels) {
+    const long long ch = (long long)blockIdx.x * 64 + threadIdx.x;
+    if (ch >= channels) return;
+    double x2 = 0.0;
+    for (long long i = 0; i < n; ++i) x2 += x[ch * n + i].energy();  // (i * i.conj()).real(), in order
+    x2 = sqrt(x2 / (double)n) + 1e-16;  // 10f64.powi(-16)
+    levels[ch] = x2;
+    if (x2 <= 0.0) return;  // SignalLevelOutOfRange: the host reports it
+    state[ch].gain = 1.0 / x2;
+    state[ch].energy_estimate = 1.0;
 }
 
 }  // namespace
@@ -131,7 +335,7 @@ __global__ void __launch_bounds__(256) nco_mix_kernel(const cpx<T>* __restrict__
 hipError_t launch_acorr(int prec, const void* x, const void* hist, void* y, size_t n, int H, int d, int K,
                         size_t channels, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    dim3 grid((unsigned)((n + kTile - 1) / kTile), (unsigned)channels);
+    dim3 grid((unsigned)((n + kOut - 1) / kOut), (unsigned)channels);
     if (prec == 0)
         hipLaunchKernelGGL(acorr_kernel<float>, grid, dim3(kTile), 0, s, (const c32*)x, (const c32*)hist, (c32*)y,
                            (long long)n, H, d, K);
@@ -166,19 +370,48 @@ hipError_t launch_acorr_energy(int prec, const void* x, const void* hist, size_t
 hipError_t launch_nco_mix(int prec, bool down, const void* x, void* y, size_t n, const double* table, uint32_t theta0,
                           uint32_t dtheta, int num_cus, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    long long blocks = ((long long)n + 255) / 256;
-    const long long cap = (long long)num_cus * 16;
-    if (blocks > cap) blocks = cap;
+    const bool a16 = (((uintptr_t)x | (uintptr_t)y) & 15) == 0;
+    const int V = prec == 0 && a16 ? 2 : 1;
+    (void)num_cus;
+    long long blocks = ((long long)n / V + 256 * kNcoU - 1) / (256 * kNcoU);
+    if (blocks < 1) blocks = 1;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     dim3 grid((unsigned)blocks);
-#define SDSP_NCO(T, D)                                                                                        \
-    hipLaunchKernelGGL((nco_mix_kernel<T, D>), grid, dim3(256), 0, s, (const cpx<T>*)x, (cpx<T>*)y, (long long)n, \
+#define SDSP_NCO(T, D, V)                                                                                        \
+    hipLaunchKernelGGL((nco_mix_kernel<T, D, V>), grid, dim3(256), 0, s, (const cpx<T>*)x, (cpx<T>*)y, (long long)n, \
                        table, theta0, dtheta)
-    if (prec == 0) {
-        if (down) SDSP_NCO(float, true); else SDSP_NCO(float, false);
+    if (prec == 0 && V == 2) {
+        if (down) SDSP_NCO(float, true, 2); else SDSP_NCO(float, false, 2);
+    } else if (prec == 0) {
+        if (down) SDSP_NCO(float, true, 1); else SDSP_NCO(float, false, 1);
     } else {
-        if (down) SDSP_NCO(double, true); else SDSP_NCO(double, false);
+        if (down) SDSP_NCO(double, true, 1); else SDSP_NCO(double, false, 1);
     }
 #undef SDSP_NCO
+    return hipGetLastError();
+}
+
+hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, size_t channels, hipStream_t s) {
+    if (n == 0 || channels == 0) return hipSuccess;
+    dim3 grid((unsigned)((channels + 63) / 64));
+    if (cplx)
+        hipLaunchKernelGGL(agc_kernel<true>, grid, dim3(64), 0, s, (const AgcSample<true>*)x, (AgcSample<true>*)y,
+                           (long long)n, (sdsp_agc_state*)state, (long long)channels);
+    else
+        hipLaunchKernelGGL(agc_kernel<false>, grid, dim3(64), 0, s, (const AgcSample<false>*)x, (AgcSample<false>*)y,
+                           (long long)n, (sdsp_agc_state*)state, (long long)channels);
+    return hipGetLastError();
+}
+
+hipError_t launch_agc_init(bool cplx, const void* x, size_t n, void* state, double* levels, size_t channels,
+                           hipStream_t s) {
+    dim3 grid((unsigned)((channels + 63) / 64));
+    if (cplx)
+        hipLaunchKernelGGL(agc_init_kernel<true>, grid, dim3(64), 0, s, (const AgcSample<true>*)x, (long long)n,
+                           (sdsp_agc_state*)state, levels, (long long)channels);
+    else
+        hipLaunchKernelGGL(agc_init_kernel<false>, grid, dim3(64), 0, s, (const AgcSample<false>*)x, (long long)n,
+                           (sdsp_agc_state*)state, levels, (long long)channels);
     return hipGetLastError();
 }
 

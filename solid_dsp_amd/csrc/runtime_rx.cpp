@@ -1,7 +1,9 @@
 // C-ABI runtime for the receive-chain objects next to the filter path
-// (SURVEY §8f rows 3-4): AutoCorrelator (src/filter/auto_correlator/mod.rs)
-// and NCO (src/nco/mod.rs).  The sample streams run in kern_rx.hip; the NCO's
-// scalar phase/frequency registers are host state, as in the reference.
+// (SURVEY §8f rows 3-4): AutoCorrelator (src/filter/auto_correlator/mod.rs),
+// NCO (src/nco/mod.rs) and the AGC bank (src/auto_gain_control/mod.rs).  The
+// sample streams run in kern_rx.hip; the NCO's scalar phase/frequency registers
+// are host state, as in the reference; the AGC state lives on the device (the
+// recurrence updates it every sample) with a host copy for setters and getters.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -409,6 +411,258 @@ int sdsp_nco_synchronize(sdsp_nco* h) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     Guard g(h->device);
     R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// AGC bank (src/auto_gain_control/mod.rs:97-677)
+// ===========================================================================
+struct sdsp_agc {
+    int device = 0;
+    size_t channels = 1;
+    std::vector<sdsp_agc_state> host;  // valid when host_valid; the device copy is authoritative after a run
+    bool host_valid = true;
+    DevBuf d_state, d_levels, stage_in, stage_out;
+    hipStream_t stream = nullptr, last = nullptr;
+};
+
+namespace {
+sdsp_agc_state agc_new_state() {  // AGC::new  :136-149
+    sdsp_agc_state s{};
+    s.gain = 1.0;
+    s.scale = 1.0;
+    s.bandwidth = 0.1;
+    s.alpha = 0.1;
+    s.energy_estimate = 1.0;
+    s.lock = 0;
+    s.squelch_mode = SDSP_SQUELCH_DISABLED;
+    s.squelch_threshold = 0.0;
+    s.squelch_timeout = 100;
+    s.squelch_timer = 0;
+    return s;
+}
+int agc_pull(sdsp_agc* h) {
+    if (h->host_valid) return SDSP_OK;
+    if (h->last) R_TRY(hipStreamSynchronize(h->last), "sync");
+    R_TRY(hipMemcpy(h->host.data(), h->d_state.p, h->channels * sizeof(sdsp_agc_state), hipMemcpyDeviceToHost),
+          "state D2H");
+    h->host_valid = true;
+    return SDSP_OK;
+}
+int agc_push(sdsp_agc* h) {
+    if (h->last) R_TRY(hipStreamSynchronize(h->last), "sync");
+    R_TRY(hipMemcpy(h->d_state.p, h->host.data(), h->channels * sizeof(sdsp_agc_state), hipMemcpyHostToDevice),
+          "state H2D");
+    return SDSP_OK;
+}
+// read-modify-write every channel's state
+template <typename F> int agc_update(sdsp_agc* h, F f) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    int st = agc_pull(h);
+    if (st) return st;
+    for (auto& s : h->host) f(s);
+    return agc_push(h);
+}
+size_t agc_bytes(int sample_type) { return sample_type == 1 ? 16 : 8; }
+}  // namespace
+
+extern "C" {
+
+int sdsp_agc_create(sdsp_agc** out, size_t channels, int device) {
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    *out = nullptr;
+    if (channels == 0) {
+        set_error("channels must be > 0");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    int st = check_gfx950(device, nullptr);
+    if (st) return st;
+    Guard g(device);
+    auto* h = new sdsp_agc();
+    h->device = device;
+    h->channels = channels;
+    h->host.assign(channels, agc_new_state());
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        set_error("hipStreamCreate failed");
+        return SDSP_E_DEVICE;
+    }
+    if (h->d_state.ensure(channels * sizeof(sdsp_agc_state)) != hipSuccess || (st = agc_push(h)) != SDSP_OK) {
+        sdsp_agc_destroy(h);
+        set_error("AGC state upload failed");
+        return st ? st : SDSP_E_DEVICE;
+    }
+    *out = h;
+    return SDSP_OK;
+}
+
+void sdsp_agc_destroy(sdsp_agc* h) {
+    if (!h) return;
+    {
+        Guard g(h->device);
+        if (h->last) (void)hipStreamSynchronize(h->last);
+        if (h->stream) {
+            (void)hipStreamSynchronize(h->stream);
+            (void)hipStreamDestroy(h->stream);
+        }
+        h->d_state.release();
+        h->d_levels.release();
+        h->stage_in.release();
+        h->stage_out.release();
+    }
+    delete h;
+}
+
+size_t sdsp_agc_channels(const sdsp_agc* h) { return h ? h->channels : 0; }
+
+int sdsp_agc_reset(sdsp_agc* h) {  // :178-188 (squelch stays enabled if it was on)
+    return agc_update(h, [](sdsp_agc_state& s) {
+        s.gain = 1.0;
+        s.energy_estimate = 1.0;
+        s.lock = 0;
+        s.squelch_mode = s.squelch_mode == SDSP_SQUELCH_DISABLED ? SDSP_SQUELCH_DISABLED : SDSP_SQUELCH_ENABLED;
+    });
+}
+
+int sdsp_agc_execute_block_device(sdsp_agc* h, int sample_type, const void* d_in, size_t n, void* d_out,
+                                  void* stream) {
+    if (!h || (sample_type != 0 && sample_type != 1) || (n && (!d_in || !d_out))) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) return SDSP_OK;
+    Guard g(h->device);
+    hipStream_t s = pick(stream, h->stream);
+    if (h->last && h->last != s) R_TRY(hipStreamSynchronize(h->last), "sync");  // state hand-off between streams
+    R_TRY(launch_agc(sample_type == 1, d_in, d_out, n, h->d_state.p, h->channels, s), "agc");
+    h->last = s;
+    h->host_valid = false;
+    return SDSP_OK;
+}
+
+int sdsp_agc_execute_block(sdsp_agc* h, int sample_type, const void* in, size_t n, void* out) {
+    if (!h || (sample_type != 0 && sample_type != 1) || (n && (!in || !out))) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) return SDSP_OK;
+    Guard g(h->device);
+    const size_t bytes = h->channels * n * agc_bytes(sample_type);
+    R_TRY(h->stage_in.ensure(bytes), "stage in");
+    R_TRY(h->stage_out.ensure(bytes), "stage out");
+    R_TRY(hipMemcpyAsync(h->stage_in.p, in, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    int st = sdsp_agc_execute_block_device(h, sample_type, h->stage_in.p, n, h->stage_out.p, h->stream);
+    if (st) return st;
+    R_TRY(hipMemcpyAsync(out, h->stage_out.p, bytes, hipMemcpyDeviceToHost, h->stream), "D2H");
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    return SDSP_OK;
+}
+
+int sdsp_agc_init(sdsp_agc* h, int sample_type, const void* in, size_t n, double* levels) {
+    if (!h || (sample_type != 0 && sample_type != 1) || (n && !in)) return SDSP_E_INVALID_ARGUMENT;
+    if (n == 0) {
+        set_error("AGC Error Need more than 0 Samples to operate");
+        return SDSP_E_AGC_SAMPLES_TOO_LOW;
+    }
+    Guard g(h->device);
+    int st = agc_pull(h);
+    if (st) return st;
+    const size_t bytes = h->channels * n * agc_bytes(sample_type);
+    R_TRY(h->stage_in.ensure(bytes), "stage in");
+    R_TRY(h->d_levels.ensure(h->channels * 8), "levels");
+    if (h->last && h->last != h->stream) R_TRY(hipStreamSynchronize(h->last), "sync");
+    R_TRY(hipMemcpyAsync(h->stage_in.p, in, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
+    R_TRY(launch_agc_init(sample_type == 1, h->stage_in.p, n, h->d_state.p, (double*)h->d_levels.p, h->channels,
+                          h->stream),
+          "agc init");
+    std::vector<double> lv(h->channels);
+    R_TRY(hipMemcpyAsync(lv.data(), h->d_levels.p, h->channels * 8, hipMemcpyDeviceToHost, h->stream), "D2H");
+    R_TRY(hipStreamSynchronize(h->stream), "sync");
+    h->last = h->stream;
+    h->host_valid = false;
+    if (levels) std::memcpy(levels, lv.data(), h->channels * 8);
+    for (double l : lv)
+        if (!(l > 0.0)) {
+            set_error("AGC Error Level is too low (0, inf)");
+            return SDSP_E_AGC_SIGNAL_LEVEL_OUT_OF_RANGE;
+        }
+    return SDSP_OK;
+}
+
+int sdsp_agc_lock(sdsp_agc* h) { return agc_update(h, [](sdsp_agc_state& s) { s.lock = 1; }); }
+int sdsp_agc_unlock(sdsp_agc* h) { return agc_update(h, [](sdsp_agc_state& s) { s.lock = 0; }); }
+
+int sdsp_agc_set_bandwidth(sdsp_agc* h, double bw) {  // :374-386
+    if (!(bw >= 0.0 && bw <= 1.0)) {
+        set_error("AGC Error Bandwidth not in range [0, 1]");
+        return h ? SDSP_E_AGC_BANDWIDTH_OUT_OF_RANGE : SDSP_E_INVALID_ARGUMENT;
+    }
+    return agc_update(h, [bw](sdsp_agc_state& s) {
+        s.bandwidth = bw;
+        s.alpha = bw;
+    });
+}
+int sdsp_agc_set_signal_level(sdsp_agc* h, double level) {  // :416-428
+    if (level <= 0.0) {
+        set_error("AGC Error Level is too low (0, inf)");
+        return h ? SDSP_E_AGC_SIGNAL_LEVEL_OUT_OF_RANGE : SDSP_E_INVALID_ARGUMENT;
+    }
+    return agc_update(h, [level](sdsp_agc_state& s) {
+        s.gain = 1.0 / level;
+        s.energy_estimate = 1.0;
+    });
+}
+int sdsp_agc_set_rssi(sdsp_agc* h, double rssi) {  // :458-466
+    return agc_update(h, [rssi](sdsp_agc_state& s) {
+        s.gain = std::pow(10.0, -rssi / 20.0);
+        if (s.gain < 1e-16) s.gain = 1e-16;
+        s.energy_estimate = 1.0;
+    });
+}
+int sdsp_agc_set_gain(sdsp_agc* h, double gain) {  // :497-504
+    if (gain <= 0.0) {
+        set_error("AGC Error Gain is below Threshold (0, inf)");
+        return h ? SDSP_E_AGC_GAIN_BELOW_THRESHOLD : SDSP_E_INVALID_ARGUMENT;
+    }
+    return agc_update(h, [gain](sdsp_agc_state& s) { s.gain = gain; });
+}
+int sdsp_agc_set_scale(sdsp_agc* h, double scale) {  // :535-542
+    if (scale <= 0.0) {
+        set_error("AGC Error Scale is below Threshold (0, inf)");
+        return h ? SDSP_E_AGC_SCALE_BELOW_THRESHOLD : SDSP_E_INVALID_ARGUMENT;
+    }
+    return agc_update(h, [scale](sdsp_agc_state& s) { s.scale = scale; });
+}
+int sdsp_agc_squelch_enable(sdsp_agc* h) {
+    return agc_update(h, [](sdsp_agc_state& s) { s.squelch_mode = SDSP_SQUELCH_ENABLED; });
+}
+int sdsp_agc_squelch_disable(sdsp_agc* h) {
+    return agc_update(h, [](sdsp_agc_state& s) { s.squelch_mode = SDSP_SQUELCH_DISABLED; });
+}
+int sdsp_agc_squelch_set_threshold(sdsp_agc* h, double threshold) {
+    return agc_update(h, [threshold](sdsp_agc_state& s) { s.squelch_threshold = threshold; });
+}
+int sdsp_agc_squelch_set_timeout(sdsp_agc* h, uint64_t timeout) {
+    return agc_update(h, [timeout](sdsp_agc_state& s) { s.squelch_timeout = timeout; });
+}
+
+int sdsp_agc_get_state(sdsp_agc* h, size_t channel, sdsp_agc_state* st) {
+    if (!h || !st || channel >= h->channels) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    int r = agc_pull(h);
+    if (r) return r;
+    *st = h->host[channel];
+    return SDSP_OK;
+}
+int sdsp_agc_set_state(sdsp_agc* h, size_t channel, const sdsp_agc_state* st) {
+    if (!h || !st || channel >= h->channels) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    int r = agc_pull(h);
+    if (r) return r;
+    h->host[channel] = *st;
+    return agc_push(h);
+}
+int sdsp_agc_synchronize(sdsp_agc* h) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    Guard g(h->device);
+    if (h->last) R_TRY(hipStreamSynchronize(h->last), "sync");
     return SDSP_OK;
 }
 

@@ -165,6 +165,11 @@ hipError_t launch_acorr_energy(int prec, const void* x, const void* hist, size_t
 // NCO mix_up / mix_down over a block (kern_rx.hip): theta_i = theta0 + i dtheta (u32)
 hipError_t launch_nco_mix(int prec, bool down, const void* x, void* y, size_t n, const double* table, uint32_t theta0,
                           uint32_t dtheta, int num_cus, hipStream_t s);
+// AGC bank (src/auto_gain_control/mod.rs): state is sdsp_agc_state[channels] in
+// device memory; cplx = Complex<f64> samples, else f64
+hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, size_t channels, hipStream_t s);
+hipError_t launch_agc_init(bool cplx, const void* x, size_t n, void* state, double* levels, size_t channels,
+                           hipStream_t s);
 
 hipError_t launch_bw_copy(const void* a, void* b, size_t bytes, int num_cus, hipStream_t s);
 hipError_t launch_synth_f32(float* out, uint64_t seed, uint64_t channel, uint64_t start, size_t count,

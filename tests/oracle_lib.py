@@ -107,6 +107,24 @@ def lib():
         "orc_nco_pll_step": (None, [vp, C.c_double]),
         "orc_nco_step": (None, [vp]),
         "orc_nco_mix_block": (None, [vp, C.c_int, dp, sz, dp]),
+        "orc_agc_new": (vp, []),
+        "orc_agc_free": (None, [vp]),
+        "orc_agc_reset": (None, [vp]),
+        "orc_agc_execute_block": (None, [vp, C.c_int, vp, sz, vp]),
+        "orc_agc_init": (C.c_int, [vp, C.c_int, vp, sz, dp]),
+        "orc_agc_set_bandwidth": (C.c_int, [vp, C.c_double]),
+        "orc_agc_set_rssi": (None, [vp, C.c_double]),
+        "orc_agc_set_gain": (None, [vp, C.c_double]),
+        "orc_agc_set_scale": (None, [vp, C.c_double]),
+        "orc_agc_lock": (None, [vp, C.c_int]),
+        "orc_agc_squelch": (None, [vp, C.c_int]),
+        "orc_agc_squelch_set_threshold": (None, [vp, C.c_double]),
+        "orc_agc_squelch_set_timeout": (None, [vp, C.c_uint64]),
+        "orc_agc_get_gain": (C.c_double, [vp]),
+        "orc_agc_get_energy": (C.c_double, [vp]),
+        "orc_agc_get_rssi": (C.c_double, [vp]),
+        "orc_agc_get_mode": (C.c_int, [vp]),
+        "orc_agc_get_timer": (C.c_uint64, [vp]),
     }
     for name, (res, args) in list(sig.items()) + list(optional.items()):
         if not hasattr(L, name):
@@ -323,6 +341,38 @@ class Nco:
         lib().orc_nco_mix_block(self.h, int(down), x.ctypes.data_as(C.POINTER(C.c_double)), len(x),
                                 out.ctypes.data_as(C.POINTER(C.c_double)))
         return out
+
+
+class Agc:
+    """Restated AGC (oracle/sdsp_oracle_rx.cpp); samples f64 or complex128."""
+
+    def __init__(self):
+        self.h = lib().orc_agc_new()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_agc_free(self.h)
+            self.h = None
+
+    def __getattr__(self, name):
+        f = getattr(lib(), "orc_agc_" + name)
+        return lambda *a: f(self.h, *a)
+
+    def execute_block(self, x):
+        x = np.ascontiguousarray(x)
+        st = 1 if np.iscomplexobj(x) else 0
+        x = x.astype(np.complex128 if st else np.float64)
+        out = np.zeros_like(x)
+        lib().orc_agc_execute_block(self.h, st, _ptr(x), len(x), _ptr(out))
+        return out
+
+    def init(self, x):
+        x = np.ascontiguousarray(x)
+        st = 1 if np.iscomplexobj(x) else 0
+        x = x.astype(np.complex128 if st else np.float64)
+        lv = np.zeros(1)
+        rc = lib().orc_agc_init(self.h, st, _ptr(x) if len(x) else None, len(x), _dptr(lv))
+        return rc, float(lv[0])
 
 
 def synth(seed, channel, start, count, complex_=False):

@@ -115,3 +115,129 @@ def test_nco_mix_c32_tolerance_and_pll():
     o.pll_step(0.3)
     assert g.state() == o.state()
     assert g.get_frequency() == 0.0 and g.get_phase() == 0.0  # integer-division quirk (nco/mod.rs:69-91)
+
+
+# ---------------------------------------------------------------- AGC
+# The device recurrence calls the gfx950 f64 exp / log / log10 (not glibc's):
+# outputs and gains agree with the restatement to a few ulp per step, and the
+# loop is contractive, so the bound below holds over thousands of samples.
+AGC_RTOL = 1e-12
+
+
+def _doctest_signal(length=500):
+    xs = np.arange(-length // 2, length // 2, dtype=np.float64)
+    return (np.cos(xs) * 0.05 + 1j * (np.sin(xs) * 0.05)).astype(C128)
+
+
+def _agc_pair(bw, squelch=True, timeout=None, channels=1):
+    import solid_dsp_amd as sd
+    g, o = sd.AGC(channels=channels), O.Agc()
+    if squelch:
+        g.squelch_enable()
+        g.squelch_set_threshold(-30.0)
+        o.squelch(1)
+        o.squelch_set_threshold(-30.0)
+    if timeout is not None:
+        g.squelch_set_timeout(timeout)
+        o.squelch_set_timeout(timeout)
+    g.set_bandwidth(bw)
+    o.set_bandwidth(bw)
+    return g, o
+
+
+def _close(y, r):
+    return np.max(np.abs(y - r)) <= AGC_RTOL * max(np.max(np.abs(r)), 1e-300)
+
+
+def test_agc_doctests_on_device():
+    """src/auto_gain_control/mod.rs:20-41, :118-135, :157-176, :194-213, :251-271, :550-567"""
+    import solid_dsp_amd as sd
+    sig = _doctest_signal()
+    g, _ = _agc_pair(0.02)
+    y = g.execute_block(sig)
+    assert 0.98 < abs(y[-1]) < 1.02
+    assert -26.0 < g.get_rssi() < -25.5
+    g, _ = _agc_pair(0.01)
+    y = g.execute_block(sig)
+    assert g.get_signal_level() < 0.05 and g.get_gain() > 1.0
+    assert len(y) == len(sig) and np.any(y != sig) and y[0] == sig[0]
+    g.reset()
+    assert g.get_gain() == 1.0 and g.squelch_get_mode() == sd.SquelchMode.ENABLED
+    g, _ = _agc_pair(0.01)
+    assert g.execute(sig[0]) == sig[0]
+    assert g.execute(sig[1]) != sig[1]
+    g, _ = _agc_pair(0.01)
+    assert 0.04999 < g.init(sig) <= 0.05
+    a = sd.AGC()
+    assert a.get_bandwidth() == 0.1 and a.get_signal_level() == 1.0 and a.get_rssi() == 0.0
+    assert a.get_gain() == 1.0 and a.get_scale() == 1.0 and not a.is_unlocked()
+    a.lock()
+    assert a.is_unlocked()
+    a.unlock()
+    a.set_signal_level(10.0)
+    assert a.get_signal_level() == 10.0
+    a.set_rssi(-20.0)
+    assert a.get_rssi() == -20.0
+    a.set_gain(2.0)
+    a.set_scale(2.0)
+    assert a.get_gain() == 2.0 and a.get_scale() == 2.0
+    assert str(a).startswith("AGC [Gain=2.00000] [Scale=2.00000]")
+
+
+def test_agc_errors():
+    import solid_dsp_amd as sd
+    a = sd.AGC()
+    for f, v, code in ((a.set_bandwidth, 1.5, 40), (a.set_bandwidth, -0.01, 40), (a.set_signal_level, 0.0, 41),
+                       (a.set_gain, 0.0, 42), (a.set_scale, -1.0, 43)):
+        with pytest.raises(sd.AGCError) as e:
+            f(v)
+        assert e.value.code == code
+    with pytest.raises(sd.AGCError) as e:
+        a.init(np.zeros(0, C128))
+    assert e.value.code == 44
+
+
+@pytest.mark.parametrize("complex_", [True, False])
+def test_agc_vs_restatement_squelch_cycle(complex_):
+    """burst, silence past the squelch timeout, second burst: every squelch state,
+    ragged block boundaries (not multiples of the 16-sample LDS chunk)"""
+    rng = np.random.default_rng(21)
+    parts = [0.05 * rng.standard_normal(3000), 1e-9 * np.ones(4000), 0.3 * rng.standard_normal(3000)]
+    if complex_:
+        parts = [p + 1j * 0.7 * rng.standard_normal(len(p)) * (np.abs(p).mean()) for p in parts]
+    x = np.concatenate(parts)
+    g, o = _agc_pair(0.05, timeout=37)
+    for lo, hi in [(0, 1), (1, 17), (17, 4001), (4001, len(x))]:
+        y = g.execute_block(x[lo:hi])
+        r = o.execute_block(x[lo:hi])
+        assert _close(y, r), (lo, hi)
+        assert abs(g.get_gain() - o.get_gain()) <= AGC_RTOL * o.get_gain()
+        assert int(g.squelch_get_mode()) == o.get_mode()
+        assert g.state().squelch_timer == o.get_timer()
+
+
+def test_agc_bank_and_device_lock():
+    """a 70-channel bank (two 64-lane workgroups, ragged) on device buffers, then locked"""
+    import torch
+    import solid_dsp_amd as sd
+    rng = np.random.default_rng(22)
+    ch, n = 70, 2500
+    amp = 10.0 ** rng.uniform(-3, 0, ch)
+    x = ((rng.standard_normal((ch, n)) + 1j * rng.standard_normal((ch, n))) * amp[:, None]).astype(C128)
+    g = sd.AGC(channels=ch)
+    g.set_bandwidth(0.02)
+    d_in = torch.from_numpy(x).to("cuda")
+    d_out = torch.empty_like(d_in)
+    g.execute_block_device(d_in, n, d_out, complex_=True, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    y = d_out.cpu().numpy()
+    gains = g.get_gain()
+    for c in range(ch):
+        o = O.Agc()
+        o.set_bandwidth(0.02)
+        assert _close(y[c], o.execute_block(x[c])), c
+        assert abs(gains[c] - o.get_gain()) <= AGC_RTOL * o.get_gain()
+    g.lock()
+    y2 = g.execute_block(x)
+    assert np.array_equal(y2, x * gains[:, None])  # locked: out = input * gain, gain frozen
+    assert np.array_equal(g.get_gain(), gains)

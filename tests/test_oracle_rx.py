@@ -125,3 +125,103 @@ def test_nco_pll_and_bandwidth():
     n.pll_step(0.3)
     th, dt = n.state()
     assert dt == _py_constrain(0.3 * 0.04) and th == _py_constrain(0.3 * math.sqrt(0.04))
+
+
+# ---------------------------------------------------------------- AGC
+def _agc(bw, squelch=True):
+    a = O.Agc()
+    if squelch:
+        a.squelch(1)
+        a.squelch_set_threshold(-30.0)
+    assert a.set_bandwidth(bw) == 0
+    return a
+
+
+def test_agc_doctest_kats():
+    """The reference's doctests (src/auto_gain_control/mod.rs:20-41, :118-135, :157-176,
+    :194-213, :251-271, :550-567)."""
+    sig = _doctest_signal()
+    a = _agc(0.02)
+    y = a.execute_block(sig)
+    assert 0.98 < abs(y[-1]) < 1.02
+    assert -26.0 < a.get_rssi() < -25.5
+    a = _agc(0.01)
+    y = a.execute_block(sig)
+    assert 1.0 / a.get_gain() < 0.05  # get_signal_level
+    assert a.get_gain() > 1.0
+    a.reset()
+    assert a.get_gain() == 1.0
+    assert len(y) == len(sig) and np.any(y != sig) and y[0] == sig[0]
+    a = _agc(0.01)
+    assert a.execute_block(sig[:1])[0] == sig[0]
+    assert a.execute_block(sig[1:2])[0] != sig[1]
+    a = _agc(0.01)
+    rc, level = a.init(sig)
+    assert rc == 0 and 0.04999 < level <= 0.05
+
+
+def test_agc_setters_and_errors():
+    a = O.Agc()
+    assert a.get_gain() == 1.0 and a.get_rssi() == 0.0  # -0.0 == 0.0
+    a.set_rssi(-20.0)
+    assert a.get_rssi() == -20.0
+    assert a.set_bandwidth(1.5) == 40 and a.set_bandwidth(-0.1) == 40
+    assert a.init(np.zeros(0, np.complex128))[0] == 44
+    a.set_rssi(400.0)  # gain clamps at 1e-16
+    assert a.get_gain() == 1e-16
+
+
+def _py_agc(x, bw, thr=None, timeout=100, lock=False, scale=1.0):
+    """Literal restatement of execute / update_squelch_mode in Python floats."""
+    gain, E, alpha, mode, timer = 1.0, 1.0, bw, ("EN" if thr is not None else "DIS"), 0
+    out = []
+    for v in x:
+        o = v * gain
+        ee = (o.conjugate() * o).real
+        E = (1.0 - alpha) * E + ee * alpha
+        if lock:
+            out.append(o)
+            continue
+        if E > 0.000001:
+            gain *= math.exp(-0.5 * alpha * math.log(E))
+        gain = min(gain, 1000000.0)
+        if mode != "DIS":
+            hi = math.log10(gain) * -20.0 > thr
+            if mode == "EN":
+                mode = "RISE" if hi else "EN"
+            elif mode == "RISE":
+                mode = "HI" if hi else "FALL"
+            elif mode == "HI":
+                mode = "HI" if hi else "FALL"
+            elif mode == "FALL":
+                timer = timeout
+                mode = "HI" if hi else "LO"
+            elif mode == "LO":
+                timer -= 1
+                mode = "TO" if timer == 0 else ("HI" if hi else "LO")
+            elif mode == "TO":
+                mode = "EN"
+        out.append(v if mode == "EN" else o * scale)
+    return np.array(out), gain, E
+
+
+def test_agc_matches_literal_python():
+    """bit-identical to a literal Python restatement (same libm), squelch cycling
+    through every state: a burst, silence past the timeout, a second burst."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([0.05 * (rng.standard_normal(300) + 1j * rng.standard_normal(300)),
+                        1e-9 * np.ones(400, np.complex128),
+                        0.2 * (rng.standard_normal(300) + 1j * rng.standard_normal(300))])
+    for thr in (-30.0, None):
+        a = _agc(0.05, squelch=thr is not None)
+        if thr is not None:
+            a.squelch_set_timeout(37)
+        y = a.execute_block(x)
+        ref, g, e = _py_agc(x, 0.05, thr, timeout=37)
+        assert y.tobytes() == ref.astype(np.complex128).tobytes()
+        assert a.get_gain() == g and a.get_energy() == e
+    a = O.Agc()
+    a.lock(1)
+    xr = rng.standard_normal(100)
+    ref, g, e = _py_agc(xr.astype(np.float64), 0.1, lock=True)
+    assert a.execute_block(xr).tobytes() == ref.astype(np.float64).tobytes()
