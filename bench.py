@@ -16,6 +16,7 @@ SURVEY §8f rows (build-defined cases, same parity + measurement fields):
   6  AutoCorrelator(64, 16), c32, 2^29 samples
   7  NCO mix_down, c32, 2^30 samples
   8  batched 2^20-point forward FFT (four-step), c32, 2^28 samples
+  9  AGC bank, Complex<f64>, 2^18 channels x 2^10 samples
 
 With N ranks each rank processes its own independent channel(s) (weak
 scaling, no collective in the timed region); RCCL is used afterwards only for
@@ -42,7 +43,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5, 6, 7, 8])
+    p.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5, 6, 7, 8, 9])
     p.add_argument("--log2n", type=int, default=30, help="samples per GPU per step (configs 2-4)")
     p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"], help="config 2 kernel")
     p.add_argument("--cpu-samples", type=int, default=None,
@@ -523,9 +524,74 @@ class Cfg8FFT:
             L.orc_fft_free(h)
 
 
-WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT}
+class Cfg9AGC:
+    """AGC bank: 2^18 independent AGC(bandwidth 0.02, squelch -30 dB) channels x 2^10
+    Complex<f64> samples (src/auto_gain_control/mod.rs:214-285); one lane per channel."""
+    metric = "Msamples/sec AGC execute_block, Complex<f64>, 2^18 channels; % HBM roofline"
+
+    def __init__(self, args, rank, dev, torch, sd):
+        self.ch, self.n = 1 << 18, 1 << 10
+        self.f = self._make(sd, dev)
+        total = self.ch * self.n
+        self.d_in = torch.empty(total, dtype=torch.complex128, device="cuda")
+        self.d_out = torch.empty(total, dtype=torch.complex128, device="cuda")
+        tmp = torch.empty(2 * total, dtype=torch.float32, device="cuda")
+        sd.lib().sdsp_synth_f32_device(tmp.data_ptr(), SEED, rank, 0, 2 * total, torch.cuda.current_stream().cuda_stream)
+        self.d_in.copy_(torch.view_as_complex(tmp.view(-1, 2).to(torch.float64) * 0.05))
+        del tmp
+        self.samples_per_step = total
+        self.bytes_per_step = 32 * total
+        self.dtype = "c64 (f64 gain recurrence with exp/ln/log10 per sample)"
+        self.kernel = "agc_kernel<true> (one lane per channel, 16-sample LDS runs)"
+        self.parity_check = "max |y - ref| / max |ref| over the first 64 channels vs the f64 restatement (tolerance 1e-12)"
+        self.workload = "cfg9: AGC(bw 0.02, squelch -30 dB) bank, 2^18 channels x 2^10 Complex<f64> samples"
+        self.algo_name = "agc"
+
+    @staticmethod
+    def _make(sd, dev=0):
+        f = sd.AGC(channels=1 << 18, device=dev)
+        f.set_bandwidth(0.02)
+        f.squelch_enable()
+        f.squelch_set_threshold(-30.0)
+        return f
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, complex_=True, stream=stream)
+
+    def parity(self, stream, rng):
+        import oracle_lib as O
+        import torch
+        import solid_dsp_amd as sd
+        g = self._make(sd)
+        g.execute_block_device(self.d_in, self.n, self.d_out, complex_=True, stream=stream)
+        torch.cuda.synchronize()
+        m = 64 * self.n
+        x = self.d_in[:m].cpu().numpy().reshape(64, self.n)
+        y = self.d_out[:m].cpu().numpy().reshape(64, self.n)
+        worst = 0.0
+        for c in range(64):
+            o = O.Agc()
+            o.set_bandwidth(0.02)
+            o.squelch(1)
+            o.squelch_set_threshold(-30.0)
+            r = o.execute_block(x[c])
+            worst = max(worst, float(np.max(np.abs(y[c] - r)) / np.max(np.abs(r))))
+        return worst
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = (O.synth(SEED, 0, 0, CPU_CHUNK // 4, complex_=True).astype(np.complex128) * 0.05)
+        o = O.Agc()
+        o.set_bandwidth(0.02)
+        o.squelch(1)
+        o.squelch_set_threshold(-30.0)
+        return timed_cpu(lambda c: o.execute_block(x), "AGC<Complex<f64>> restatement (execute per sample, "
+                         "libm exp/ln/log10)", samples, CPU_CHUNK // 4)
+
+
+WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT, 9: Cfg9AGC}
 # bounded CPU samples: about 10-20 s of single-thread work each on a current x86 host
-CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 << 25, 7: 1 << 28, 8: 1 << 24}
+CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 << 25, 7: 1 << 28, 8: 1 << 24, 9: 1 << 25}
 CPU_CHUNK = 1 << 22
 
 

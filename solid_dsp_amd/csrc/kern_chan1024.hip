@@ -21,6 +21,8 @@
 // Arithmetic: fused multiply-add, f32; parity is the §8d tolerance against the
 // f64 restatement (tests/test_gpu_fft.py).
 #include "sdsp_device.hpp"
+#include <cstdlib>
+
 #include "sdsp_kernels.hpp"
 
 namespace sdsp {
@@ -105,10 +107,9 @@ constexpr int kFrames = kThreads / 64;   // frames per round: one FFT per wave
 constexpr int kRow = 18;
 constexpr int kBuf = 64 * kRow;
 
-// one frame's FFT by one wave: buffer holds v[p] at index p on entry,
-// natural-order X written to yf
-__device__ __forceinline__ void fft1024_wave(cf* __restrict__ buf, const cf* __restrict__ stw, int L,
-                                             cf* __restrict__ yf, bool store) {
+// P1 and P2 of one wave's 1024-point FFT: buffer holds v[p] at index p on
+// entry; on exit the P3 inputs of column c = (k2 + 16 k1) sit at buf[4 c + n0]
+__device__ __forceinline__ void fft1024_p12(cf* __restrict__ buf, const cf* __restrict__ stw, int L) {
     cf v[16];
 #pragma unroll
     for (int n2 = 0; n2 < 16; ++n2) v[n2] = buf[L + 64 * n2];
@@ -131,6 +132,13 @@ __device__ __forceinline__ void fft1024_wave(cf* __restrict__ buf, const cf* __r
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) buf[(k2 + 16 * k1) * 4 + n0] = v[k1];
     wave_sync();
+}
+
+// one frame's FFT by one wave: buffer holds v[p] at index p on entry,
+// natural-order X written to yf
+__device__ __forceinline__ void fft1024_wave(cf* __restrict__ buf, const cf* __restrict__ stw, int L,
+                                             cf* __restrict__ yf, bool store) {
+    fft1024_p12(buf, stw, L);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int c = L + 64 * j;
@@ -143,6 +151,27 @@ __device__ __forceinline__ void fft1024_wave(cf* __restrict__ buf, const cf* __r
             st_nt(yf + c + 768, a3);
         }
     }
+    wave_sync();
+}
+
+// the same FFT leaving natural-order X in buf[0, 1024)
+__device__ __forceinline__ void fft1024_wave_lds(cf* __restrict__ buf, const cf* __restrict__ stw, int L) {
+    fft1024_p12(buf, stw, L);
+    cf o[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = L + 64 * j;
+        o[j][0] = buf[c * 4 + 0];
+        o[j][1] = buf[c * 4 + 1];
+        o[j][2] = buf[c * 4 + 2];
+        o[j][3] = buf[c * 4 + 3];
+        dft4(o[j][0], o[j][1], o[j][2], o[j][3]);
+    }
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k0 = 0; k0 < 4; ++k0) buf[L + 64 * j + 256 * k0] = o[j][k0];
     wave_sync();
 }
 
@@ -236,6 +265,70 @@ chan1024_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const flo
     }
 }
 
+// Four-step pass with L = 1024, complex f32 (kern_fft.hip's fft_pass_kernel
+// semantics, FftPass in sdsp_kernels.hpp): a workgroup runs 16 transforms, one
+// per wave, on the register/LDS 1024-point FFT above.  The 16 transforms are
+// consecutive t, whose elements interleave with unit stride on the strided side
+// (S1 == 1 on input, T1 == 1 on output), so loads and stores move 128-byte runs.
+// Reverse transforms conjugate in and out.  TW: the inter-pass twiddle
+// W_Ntw^m = Th[m >> 10] * Tl[m & 1023] (Ntw = 2^20, twx = [Tl | Th], f64-derived).
+constexpr int kPassBuf = kBuf + 4;  // wave-buffer stride: 16 buffers spread over LDS banks
+
+template <bool INV, bool TW, int TPB>
+__global__ void __launch_bounds__(64 * TPB)
+fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __restrict__ tw,
+                    const cf* __restrict__ twx, long long count, long long G, long long S0, long long S1,
+                    long long Si, long long T1, long long So) {
+    // TPB = 16: 156 KB of LDS, one workgroup per CU, twiddles in LDS; TPB = 8: 74 KB,
+    // two workgroups per CU (one's loads overlap the other's FFT), twiddles via L1
+    constexpr int kT = 64 * TPB, kLog = TPB == 16 ? 4 : 3;
+    __shared__ cf stw_l[TPB == 16 ? kM : 1];
+    __shared__ cf sbuf[TPB * kPassBuf];
+    const cf* stw = tw;
+    const int t = threadIdx.x, L = t & 63, w = t >> 6;
+    const long long t0 = (long long)blockIdx.x * TPB;
+    const long long g0 = t0 % G;
+    const long long ib = (t0 / G) * S0 + g0 * S1, ob = (t0 / G) * S0 + g0 * T1;
+    const int ntr = count - t0 < TPB ? (int)(count - t0) : TPB;
+    if constexpr (TPB == 16) {
+        stw_l[t] = tw[t];
+        stw = stw_l;
+    }
+    cf v[16];
+    const bool cfast = S1 == 1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = t + kT * k;
+        const int c = cfast ? (e & (TPB - 1)) : (e >> 10), i = cfast ? (e >> kLog) : (e & 1023);
+        v[k] = c < ntr ? x[ib + c * S1 + i * Si] : cf{0.0f, 0.0f};
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = t + kT * k;
+        const int c = cfast ? (e & (TPB - 1)) : (e >> 10), i = cfast ? (e >> kLog) : (e & 1023);
+        sbuf[c * kPassBuf + i] = INV ? cf{v[k].re, -v[k].im} : v[k];
+    }
+    __syncthreads();
+    fft1024_wave_lds(sbuf + w * kPassBuf, stw, L);
+    __syncthreads();
+    const bool ofast = T1 == 1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = t + kT * k;
+        const int c = ofast ? (e & (TPB - 1)) : (e >> 10), i = ofast ? (e >> kLog) : (e & 1023);
+        if (c >= ntr) continue;
+        cf r = sbuf[c * kPassBuf + i];
+        if (INV) r.im = -r.im;
+        if constexpr (TW) {
+            const unsigned m = (unsigned)(((g0 + c) * (long long)i) & ((1 << 20) - 1));
+            cf wv = cmul(twx[1024 + (m >> 10)], twx[m & 1023]);
+            if (INV) wv.im = -wv.im;
+            r = cmul(r, wv);
+        }
+        y[ob + c * T1 + i * So] = r;
+    }
+}
+
 }  // namespace
 
 // M = 1024, complex f32, K <= 8 taps per branch; false = not applicable
@@ -258,6 +351,37 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
         SDSP_CHAN(1) SDSP_CHAN(2) SDSP_CHAN(3) SDSP_CHAN(4) SDSP_CHAN(5) SDSP_CHAN(6) SDSP_CHAN(7) SDSP_CHAN(8)
     }
 #undef SDSP_CHAN
+    *err = hipGetLastError();
+    return true;
+}
+
+// four-step pass of L = 1024 on the wave FFT; false = not applicable
+bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
+    static const int tpb = [] {
+        const char* e = std::getenv("SDSP_FFT_WAVE1024");
+        const int v = e ? std::atoi(e) : 16;
+        return v == 0 || v == 8 ? v : 16;
+    }();
+    if (tpb == 0 || p.L != 1024 || p.count % tpb != 0 || p.G % tpb != 0) return false;
+    if (!(p.S1 == 1 || p.Si == 1) || !(p.T1 == 1 || p.So == 1)) return false;
+    if (p.Ntw && (p.Ntw != (1LL << 20) || !p.twx)) return false;
+    dim3 grid((unsigned)(p.count / tpb));
+#define SDSP_P1024(INV, TW, TPB)                                                                                  \
+    hipLaunchKernelGGL((fft1024_pass_kernel<INV, TW, TPB>), grid, dim3(64 * TPB), 0, s, (const cf*)p.x, (cf*)p.y, \
+                       (const cf*)p.tw, (const cf*)p.twx, p.count, p.G, p.S0, p.S1, p.Si, p.T1, p.So)
+#define SDSP_P1024_T(TPB)                                                                 \
+    if (p.inverse) {                                                                      \
+        if (p.Ntw) SDSP_P1024(true, true, TPB); else SDSP_P1024(true, false, TPB);        \
+    } else {                                                                              \
+        if (p.Ntw) SDSP_P1024(false, true, TPB); else SDSP_P1024(false, false, TPB);      \
+    }
+    if (tpb == 16) {
+        SDSP_P1024_T(16)
+    } else {
+        SDSP_P1024_T(8)
+    }
+#undef SDSP_P1024_T
+#undef SDSP_P1024
     *err = hipGetLastError();
     return true;
 }

@@ -267,6 +267,8 @@ hipError_t launch_fft_pass_t(const FftPass& p, hipStream_t s) {
 
 hipError_t launch_fft_pass(bool f64, const FftPass& p, hipStream_t s) {
     if (p.count == 0) return hipSuccess;
+    hipError_t err;
+    if (!f64 && try_launch_fft1024_pass(p, s, &err)) return err;  // L = 1024 on the wave FFT
     return f64 ? launch_fft_pass_t<double>(p, s) : launch_fft_pass_t<float>(p, s);
 }
 

@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(256) nco_mix_kernel(const cpx<T>* __restrict__
 }
 
 // ---------------------------------------------------------------- AGC
-constexpr int kAgcS = 16;  // samples per channel per LDS chunk
+constexpr int kAgcS = 8;  // samples per channel per LDS chunk
 
 template <bool CPLX> struct AgcSample;
 template <> struct AgcSample<false> {
@@ -282,7 +282,7 @@ __device__ __forceinline__ AgcSample<CPLX> agc_execute(sdsp_agc_state& s, AgcSam
 }
 
 template <bool CPLX>
-__global__ void __launch_bounds__(64) agc_kernel(const AgcSample<CPLX>* __restrict__ x, AgcSample<CPLX>* __restrict__ y,
+__global__ void __launch_bounds__(64, 4) agc_kernel(const AgcSample<CPLX>* __restrict__ x, AgcSample<CPLX>* __restrict__ y,
                                                  long long n, sdsp_agc_state* __restrict__ state, long long channels) {
     __shared__ AgcSample<CPLX> buf[64 * (kAgcS + 1)];  // row per channel, one spare slot
     const int t = threadIdx.x;

@@ -85,7 +85,7 @@ namespace {
 struct Pow2Plan {
     size_t N = 0;
     int logN = 0, l1 = 0, l2 = 0;
-    DevBuf tw, tw1, tw2;
+    DevBuf tw, tw1, tw2, twx;
     bool four_step() const { return N > 4096; }
     int build(size_t n, bool f64) {
         N = n;
@@ -95,7 +95,21 @@ struct Pow2Plan {
         l2 = logN - l1;
         int st = make_twiddles(tw1, (size_t)1 << l1, f64);
         if (st) return st;
-        return make_twiddles(tw2, (size_t)1 << l2, f64);
+        st = make_twiddles(tw2, (size_t)1 << l2, f64);
+        if (st || f64 || l1 != 10 || l2 != 10) return st;
+        // 2^20 = 1024 x 1024, complex f32: the wave-FFT passes take the inter-pass
+        // twiddle W_N^m as Th[m >> 10] * Tl[m & 1023] (each from f64)
+        std::vector<float> t(4 * 1024);
+        for (int j = 0; j < 1024; ++j) {
+            const double a = -2.0 * M_PI * (double)j / (double)N, b = -2.0 * M_PI * (double)j * 1024.0 / (double)N;
+            t[2 * j] = (float)std::cos(a);
+            t[2 * j + 1] = (float)std::sin(a);
+            t[2048 + 2 * j] = (float)std::cos(b);
+            t[2048 + 2 * j + 1] = (float)std::sin(b);
+        }
+        F_TRY(twx.ensure(t.size() * 4), "alloc twiddles");
+        F_TRY(hipMemcpy(twx.p, t.data(), t.size() * 4, hipMemcpyHostToDevice), "copy twiddles");
+        return SDSP_OK;
     }
     // in -> out (may alias); tmp: batch * N samples when four_step()
     hipError_t run(bool f64, const void* in, void* out, void* tmp, size_t batch, bool inverse, hipStream_t s) const {
@@ -105,7 +119,7 @@ struct Pow2Plan {
         }
         const long long n = (long long)N, N1 = 1LL << l1, N2 = 1LL << l2;
         // pass 1: columns n2 (length N1, stride N2) -> tmp[k1][n2] * W_N^(n2 k1)
-        FftPass p1{in, tmp, tw1.p, (int)N1, l1, (long long)batch * N2, N2, n, 1, N2, 1, N2, n, inverse};
+        FftPass p1{in, tmp, tw1.p, (int)N1, l1, (long long)batch * N2, N2, n, 1, N2, 1, N2, n, inverse, twx.p};
         hipError_t e = launch_fft_pass(f64, p1, s);
         if (e != hipSuccess) return e;
         // pass 2: rows k1 (length N2) -> out[k1 + N1 k2]
@@ -252,6 +266,7 @@ void sdsp_fft_destroy(sdsp_fft* h) {
         h->p2.tw.release();
         h->p2.tw1.release();
         h->p2.tw2.release();
+        h->p2.twx.release();
         h->chirp.release();
         h->spec.release();
         h->work.release();

@@ -122,7 +122,10 @@ struct FftPass {
     int L, logL;
     long long count, G, S0, S1, Si, T1, So, Ntw;
     bool inverse;
+    const void* twx = nullptr;  // c32 [Tl | Th] inter-pass twiddle tables when Ntw = 2^20 (L = 1024 path)
 };
+// L = 1024, complex f32 pass on the wave FFT (kern_chan1024.hip); false = not applicable
+bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err);
 hipError_t launch_fft_pass(bool f64, const FftPass& p, hipStream_t s);
 // Bluestein steps: 0 chirp in (x[N] -> a[M], zero padded), 1 a *= B, 2 chirp out (a -> y[N])
 hipError_t launch_bluestein(bool f64, int step, const void* in, void* out, const void* w_or_B, long long N, long long M,
