@@ -395,7 +395,7 @@ class Cfg6ACorr:
         self.samples_per_step = self.n
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (complex-f32 products and sums, f64 energy)"
-        self.kernel = "acorr_kernel<float> (LDS-staged conj products, 256 outputs per workgroup) + energy + history"
+        self.kernel = "acorr_kernel<float> (LDS-staged conj products, 2048 outputs per workgroup, 8 per lane) + energy + history"
         self.parity_check = "bit mismatches vs the c32 restatement over the first 2^20 outputs (must be 0)"
         self.workload = f"cfg6: AutoCorrelator(64, 16), c32, 2^{int(np.log2(self.n))} samples per channel"
         self.algo_name = "acorr"
@@ -493,7 +493,7 @@ class Cfg8FFT:
         # plan makes two passes, so its floor is 2x this
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (complex-f32 butterflies, f64-derived twiddles)"
-        self.kernel = f"fft_pass_kernel<float> x2 (four-step 1024 x 1024, {self.f.method})"
+        self.kernel = "fft1024_pass_kernel x2 (four-step 1024 x 1024 on the wave-level register FFT, 16 transforms per workgroup)"
         self.parity_check = "rel_rms of transform 0 vs numpy f64 (tolerance 5e-6)"
         self.workload = f"cfg8: {self.batch} x 2^20-point forward FFT, c32, out of place"
         self.algo_name = "fft"
@@ -542,7 +542,7 @@ class Cfg9AGC:
         self.samples_per_step = total
         self.bytes_per_step = 32 * total
         self.dtype = "c64 (f64 gain recurrence with exp/ln/log10 per sample)"
-        self.kernel = "agc_kernel<true> (one lane per channel, 16-sample LDS runs)"
+        self.kernel = "agc_kernel<true> (one lane per channel, 8-sample LDS runs)"
         self.parity_check = "max |y - ref| / max |ref| over the first 64 channels vs the f64 restatement (tolerance 1e-12)"
         self.workload = "cfg9: AGC(bw 0.02, squelch -30 dB) bank, 2^18 channels x 2^10 Complex<f64> samples"
         self.algo_name = "agc"

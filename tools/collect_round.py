@@ -14,7 +14,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = {2: ("fir_ols4096_pk_kernel", "fft"), 3: ("sos_wscan_kernel", "scan"),
           4: ("decim_poly_kernel", "fma"), 5: ("chan1024_kernel", "chan"),
-          6: ("acorr_kernel", "acorr"), 7: ("nco_mix_kernel", "nco")}
+          6: ("acorr_kernel", "acorr"), 7: ("nco_mix_kernel", "nco"), 9: ("agc_kernel", "agc")}
 
 
 def main():
