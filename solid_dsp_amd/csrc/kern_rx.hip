@@ -10,7 +10,7 @@
 // With K = max(W - d, 0) the sum is
 //     y[n] = (((0 + p[n]) + p[n-1]) + ...) + p[n-K+1],   p[m] = x[m] * conj(x[m-d]),
 // the zero-product terms j >= K leave the sum unchanged (it starts at +0 and is
-// never -0).  Each workgroup owns 2048 consecutive outputs (8 per lane); p over the window the
+// never -0).  Each one-wave workgroup owns 512 consecutive outputs (8 per lane); p over the window the
 // outputs need is built once in LDS (one num-complex product per input, the
 // reference's rounding) and every lane adds its K terms newest first, in chunks
 // of kChunk so W is unbounded.  Bit-identical to the restatement at the handle's
@@ -38,10 +38,10 @@ namespace sdsp {
 
 namespace {
 
-constexpr int kTile = 256;           // lanes per workgroup
+constexpr int kTile = 64;            // lanes per workgroup (one wave)
 constexpr int kR = 8;                // consecutive outputs per lane
 constexpr int kOut = kTile * kR;     // outputs per workgroup
-constexpr int kChunk = 1024;         // j-terms staged per pass
+constexpr int kChunk = 256;          // j-terms staged per pass
 // one spare slot per 8: lane t reads slot 8t + o, i.e. LDS element 9t + ..., so the
 // 32 (c32) or 16 (c64) lanes of one LDS cycle hit distinct banks
 __host__ __device__ constexpr int pad8(int s) { return s + (s >> 3); }
@@ -126,14 +126,26 @@ __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__
                 if (r - q >= 0 && r - q < cj) acc[r] = add_(acc[r], v);
         };
         if (cj >= kR) {
-            for (int q = kR - 1; q >= 0; --q) edge(q);           // head: r >= q
+            // head q = kR-1 .. 0: accumulators r >= q (compile-time masks)
+#pragma unroll
+            for (int q = kR - 1; q >= 0; --q) {
+                const cpx<T> v = p[pad8(s0 + q)];
+#pragma unroll
+                for (int r = q; r < kR; ++r) acc[r] = add_(acc[r], v);
+            }
 #pragma unroll 4
             for (int q = -1; q > kR - 1 - cj; --q) {              // body: every r
                 const cpx<T> v = p[pad8(s0 + q)];
 #pragma unroll
                 for (int r = 0; r < kR; ++r) acc[r] = add_(acc[r], v);
             }
-            for (int q = kR - 1 - cj; q > -cj; --q) edge(q);     // tail: r - q < cj
+            // tail q = kR-1-cj-u (u = 0 .. kR-2): accumulators r < kR-1-u
+#pragma unroll
+            for (int u = 0; u < kR - 1; ++u) {
+                const cpx<T> v = p[pad8(s0 + kR - 1 - cj - u)];
+#pragma unroll
+                for (int r = 0; r < kR - 1 - u; ++r) acc[r] = add_(acc[r], v);
+            }
         } else {
             for (int q = kR - 1; q > -cj; --q) edge(q);
         }
