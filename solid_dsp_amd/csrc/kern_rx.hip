@@ -255,13 +255,24 @@ template <> struct AgcSample<true> {
     __device__ AgcSample scaled(double g) const { return {re * g, im * g}; }
 };
 
+// get_rssi() > squelch_threshold  (:442-444, :632).  -20 log10(g) is decreasing
+// in g, so away from the threshold gain gthr = 10^(-threshold/20) the answer is
+// g < gthr; within 1e-6 relative of it (a log10 margin of 4e-7, far above the
+// rounding of either side) the reference expression decides.  NaN and infinite
+// operands fail both strict tests and take the reference expression too.
+__device__ __forceinline__ bool agc_rssi_exceeds(const sdsp_agc_state& s, double gthr) {
+    if (s.gain < gthr * (1.0 - 1e-6)) return true;
+    if (s.gain > gthr * (1.0 + 1e-6)) return false;
+    return log10(s.gain) * -20.0 > s.squelch_threshold;
+}
+
 // update_squelch_mode  :631-677 (usize timer wraps, as a release build does)
-__device__ __forceinline__ void agc_squelch(sdsp_agc_state& s) {
+__device__ __forceinline__ void agc_squelch(sdsp_agc_state& s, double gthr) {
     if (s.squelch_mode == SDSP_SQUELCH_DISABLED || s.squelch_mode == SDSP_SQUELCH_UNKNOWN) {
         s.squelch_mode = SDSP_SQUELCH_DISABLED;  // `_ => DISABLED`; the rssi it computes is unused
         return;
     }
-    const bool exceeded = log10(s.gain) * -20.0 > s.squelch_threshold;  // get_rssi  :442-444
+    const bool exceeded = agc_rssi_exceeds(s, gthr);
     switch (s.squelch_mode) {
         case SDSP_SQUELCH_ENABLED: s.squelch_mode = exceeded ? SDSP_SQUELCH_RISE : SDSP_SQUELCH_ENABLED; break;
         case SDSP_SQUELCH_RISE: s.squelch_mode = exceeded ? SDSP_SQUELCH_SIGNALHI : SDSP_SQUELCH_FALL; break;
@@ -282,13 +293,13 @@ __device__ __forceinline__ void agc_squelch(sdsp_agc_state& s) {
 
 // execute  :214-246
 template <bool CPLX>
-__device__ __forceinline__ AgcSample<CPLX> agc_execute(sdsp_agc_state& s, AgcSample<CPLX> in) {
+__device__ __forceinline__ AgcSample<CPLX> agc_execute(sdsp_agc_state& s, AgcSample<CPLX> in, double gthr) {
     const AgcSample<CPLX> out = in.scaled(s.gain);
     s.energy_estimate = (1.0 - s.alpha) * s.energy_estimate + out.energy() * s.alpha;
     if (s.lock) return out;
     if (s.energy_estimate > 0.000001) s.gain *= exp(-0.5 * s.alpha * log(s.energy_estimate));
     if (s.gain > 1000000.0) s.gain = 1000000.0;
-    agc_squelch(s);
+    agc_squelch(s, gthr);
     if (s.squelch_mode == SDSP_SQUELCH_ENABLED) return in;
     return out.scaled(s.scale);
 }
@@ -301,7 +312,11 @@ __global__ void __launch_bounds__(64, 4) agc_kernel(const AgcSample<CPLX>* __res
     const long long ch0 = (long long)blockIdx.x * 64;
     const long long me = ch0 + t;
     sdsp_agc_state s;
-    if (me < channels) s = state[me];
+    double gthr = 0.0;
+    if (me < channels) {
+        s = state[me];
+        gthr = pow(10.0, -s.squelch_threshold / 20.0);  // fixed for the launch (setters run between launches)
+    }
     for (long long i0 = 0; i0 < n; i0 += kAgcS) {
         const int cnt = n - i0 < kAgcS ? (int)(n - i0) : kAgcS;
 #pragma unroll
@@ -313,7 +328,7 @@ __global__ void __launch_bounds__(64, 4) agc_kernel(const AgcSample<CPLX>* __res
         if (me < channels)
             for (int j = 0; j < cnt; ++j) {
                 AgcSample<CPLX>& v = buf[t * (kAgcS + 1) + j];
-                v = agc_execute<CPLX>(s, v);
+                v = agc_execute<CPLX>(s, v, gthr);
             }
         __syncthreads();
 #pragma unroll

@@ -241,3 +241,23 @@ def test_agc_bank_and_device_lock():
     y2 = g.execute_block(x)
     assert np.array_equal(y2, x * gains[:, None])  # locked: out = input * gain, gain frozen
     assert np.array_equal(g.get_gain(), gains)
+
+
+@pytest.mark.parametrize("thr", [-20.0, -20.0 - 1e-12, -20.0 + 1e-12, -19.99999, -20.00001])
+def test_agc_squelch_at_threshold(thr):
+    """gain pinned exactly at the squelch threshold (x = 0.1, gain 10: E stays 1.0, the
+    rssi stays -20): the device's fast threshold test must defer to the reference
+    expression there, and agree with it just outside"""
+    import solid_dsp_amd as sd
+    g, o = sd.AGC(), O.Agc()
+    for a in (g, o):
+        a.set_rssi(-20.0)
+        a.squelch_set_threshold(thr)
+        a.squelch_set_timeout(5)
+    g.squelch_enable()
+    o.squelch(1)
+    x = np.full(64, 0.1)
+    y, r = g.execute_block(x), o.execute_block(x)
+    assert g.get_gain() == o.get_gain() == 10.0
+    assert int(g.squelch_get_mode()) == o.get_mode()
+    assert y.tobytes() == r.tobytes()
