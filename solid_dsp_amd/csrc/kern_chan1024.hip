@@ -284,6 +284,7 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
     constexpr int kT = 64 * TPB, kLog = TPB == 16 ? 4 : 3;
     __shared__ cf stw_l[TPB == 16 ? kM : 1];
     __shared__ cf sbuf[TPB * kPassBuf];
+    __shared__ cf ktab[TW ? TPB * 16 : 1];  // W^(64 (g0 + c) k), k = 0..15 (c-fast outputs)
     const cf* stw = tw;
     const int t = threadIdx.x, L = t & 63, w = t >> 6;
     const long long t0 = (long long)blockIdx.x * TPB;
@@ -293,6 +294,18 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
     if constexpr (TPB == 16) {
         stw_l[t] = tw[t];
         stw = stw_l;
+    }
+    // inter-pass twiddle of c-fast output k of this thread: i = (t >> kLog) + 64 k, so
+    // W^((g0 + c) i) = W^((g0 + c) (t >> kLog)) * W^(64 (g0 + c) k): one per-thread base
+    // and a 16-entry row per column, each Th * Tl from the f64-built tables
+    auto twx_at = [&](long long m) -> cf {
+        const unsigned u = (unsigned)(m & ((1 << 20) - 1));
+        return cmul(twx[1024 + (u >> 10)], twx[u & 1023]);
+    };
+    cf tbase = cf{1.0f, 0.0f};
+    if constexpr (TW) {
+        if (t < TPB * 16) ktab[t] = twx_at(64 * (g0 + (t >> 4)) * (long long)(t & 15));
+        if (T1 == 1) tbase = twx_at((g0 + (t & (TPB - 1))) * (long long)(t >> kLog));
     }
     cf v[16];
     const bool cfast = S1 == 1;
@@ -320,8 +333,7 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
         cf r = sbuf[c * kPassBuf + i];
         if (INV) r.im = -r.im;
         if constexpr (TW) {
-            const unsigned m = (unsigned)(((g0 + c) * (long long)i) & ((1 << 20) - 1));
-            cf wv = cmul(twx[1024 + (m >> 10)], twx[m & 1023]);
+            cf wv = ofast ? cmul(tbase, ktab[c * 16 + k]) : twx_at((g0 + c) * (long long)i);
             if (INV) wv.im = -wv.im;
             r = cmul(r, wv);
         }
