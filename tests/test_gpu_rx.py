@@ -261,3 +261,26 @@ def test_agc_squelch_at_threshold(thr):
     assert g.get_gain() == o.get_gain() == 10.0
     assert int(g.squelch_get_mode()) == o.get_mode()
     assert y.tobytes() == r.tobytes()
+
+
+def test_nco_device_unaligned_and_odd():
+    """device mixing through 8-byte-aligned (not 16-byte) c32 pointers and odd lengths:
+    the kernel's one-sample-per-lane form and the ragged tail"""
+    import torch
+    import solid_dsp_amd as sd
+    rng = np.random.default_rng(14)
+    n = 100001
+    x = _rand(rng, n + 1, C64)
+    d_in = torch.from_numpy(x).to("cuda")
+    d_out = torch.zeros_like(d_in)
+    for off, m in ((1, n), (0, n), (1, 3)):
+        g, o = sd.NCO(), O.Nco()
+        for f in (g, o):
+            f.set_frequency(0.7)
+            f.set_phase(1.1)
+        g.mix_block_device(d_in[off:], m, d_out[off:], down=True, precision=0, stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        y = d_out[off:off + m].cpu().numpy()
+        r = o.mix_block(x[off:off + m].astype(C128), True)
+        assert np.linalg.norm(y - r) / np.linalg.norm(r) <= 1e-6, (off, m)
+        assert g.state() == o.state()
