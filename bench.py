@@ -139,8 +139,8 @@ class Cfg2FIR:
         self.samples_per_step = self.n
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (f32 taps x complex-f32 samples, f32 accumulate)"
-        self.kernel = {"fft": "fir_ols4096_pk_kernel (packed-FP32 overlap-save N=4096, 16-byte rows, 16 segments "
-                              "per workgroup) + fir_ols4096_edge_kernel (2 boundary segments)",
+        self.kernel = {"fft": "fir_ols_os_kernel (one-shot XCD-ordered packed-FP32 overlap-save N=4096, one segment "
+                              "per workgroup, 4 workgroups/CU) + fir_ols4096_edge_kernel (2 boundary segments)",
                        "exact": "fir_direct_kernel<EXACT>",
                        "fma": "fir_direct_kernel<FMA>"}[args.algo]
         self.workload = (f"cfg2: 256-tap crcf FIR, firdes_kaiser(256, 0.1, 80), scale 0.2, 2^{args.log2n} samples "

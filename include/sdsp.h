@@ -28,6 +28,12 @@
  *    the end of every call).
  *  - No CPU fallback: with no usable gfx950 device every create call returns
  *    SDSP_E_NO_DEVICE.
+ *  - Streaming calls do not filter in place: an input block that overlaps its
+ *    output block is rejected with SDSP_E_INVALID_ARGUMENT (the kernels read
+ *    each input window, and the delay-line update reads the block's tail, after
+ *    other workgroups have started writing outputs).
+ *  - Host-side state calls (reset, get/set_state, clone, set_scale) first wait
+ *    for the work an earlier *_execute_block_device queued on a caller stream.
  */
 #ifndef SDSP_H
 #define SDSP_H
@@ -51,9 +57,11 @@ typedef enum {
     SDSP_CC64 = 5  /* c64  taps, c64  samples                                  */
 } sdsp_dtype;
 
-/* Kernel selection for FIR-type handles. */
+/* Kernel selection for FIR-type and IIR handles.  A new handle uses SDSP_ALGO_EXACT:
+ * by default every result is bit-identical to the reference algorithm at the handle's
+ * precision, whatever the block size.  The fast kernels are opt-in. */
 typedef enum {
-    SDSP_ALGO_AUTO = 0,  /* FFT overlap-save for 32-bit complex when it applies, else EXACT */
+    SDSP_ALGO_AUTO = 0,  /* FFT overlap-save for 32-bit complex blocks >= 65536 samples, else EXACT */
     SDSP_ALGO_EXACT = 1, /* direct form in the reference summation order, no FMA contraction:
                             bit-identical to the reference algorithm at the handle's precision */
     SDSP_ALGO_FMA = 2,   /* direct form, same order, fused multiply-add                      */
@@ -121,27 +129,16 @@ SDSP_API int sdsp_decim_create(sdsp_fir** out, int dtype, const void* taps, size
 SDSP_API int sdsp_fir_set_channels(sdsp_fir* h, size_t channels);
 SDSP_API int sdsp_fir_set_algo(sdsp_fir* h, int algo);
 SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
-/* kernel-variant knobs (performance only; results are identical across values, except
- * SDSP_TUNE_OLS_ABLATE_NOMEM, a profiling ablation that skips HBM traffic and leaves the
- * output unwritten).  Overlap-save defaults: PACKED = 1, WIDE = 1 (16-byte accesses in the
- * packed kernel), SEGS_PER_BLOCK = 16, SCHEDULE = 2, XCD_ORDER = 1. */
+/* kernel-variant knobs: performance only, every accepted value computes the complete output
+ * (retired keys of earlier builds are rejected with SDSP_E_INVALID_ARGUMENT). */
 typedef enum {
-    SDSP_TUNE_OLS_WIDE = 1,        /* packed overlap-save: 1 (default) = 16-byte global accesses */
-    SDSP_TUNE_OLS_INTERLEAVE = 2,  /* 1 (default): segments interleaved across the persistent grid */
-    SDSP_TUNE_OLS_SCHEDULE = 3,    /* packed overlap-save HBM issue schedule: 0 loads and stores in one burst per
-                                      segment, 1 two segments of loads in flight, 2 (default) .. 10 spread over the
-                                      segment's phases (kern_fir_ols_pk.hip kLoadAt / kStoreAt tables 1..9) */
-    SDSP_TUNE_OLS_ABLATE_NOMEM = 4,
-    SDSP_TUNE_OLS_XCD_ORDER = 5,   /* packed overlap-save: 1 (default) = each XCD streams one contiguous part */
     SDSP_TUNE_DECIM_SEG = 6,     /* FMA decimator: outputs per lane group (0 = automatic) */
     SDSP_TUNE_IIR_WAVE_SCAN = 7, /* IIR scan kernel: 0 = block scan, 1 (default) = wave scan with 256-byte chunks,
                                     2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */
     SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: 1 (default) = streaming M=1024 kernel where it applies, 0 = per-frame */
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
-    SDSP_TUNE_OLS_NONTEMPORAL = 10, /* overlap-save streaming loads (bit 0) / stores (bit 1) */
-    SDSP_TUNE_OLS_WAVE = 11,        /* overlap-save: 1 = wave-per-segment N=1024 kernel (L <= 257) */
-    SDSP_TUNE_OLS_PACKED = 12,      /* overlap-save: interior segments in packed-FP32 arithmetic (L <= 1025) */
-    SDSP_TUNE_OLS_SEGS_PER_BLOCK = 13 /* packed overlap-save: 0 = persistent grid, k = k consecutive segments per workgroup */
+    SDSP_TUNE_OLS_KERNEL = 14    /* overlap-save interior segments (16-byte aligned rows): 0 (default) one-shot
+                                    XCD-ordered kernel, 1 persistent packed kernel (L <= 1025), 2 scalar kernel */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */

@@ -281,11 +281,35 @@ def dptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
-def device_ptr(t) -> int:
-    """Raw device pointer of a torch tensor / int (torch is plumbing only)."""
+def device_ptr(t, dtype=None, count=None, device=None, what="buffer") -> int:
+    """Raw device pointer of a torch tensor or int (torch is plumbing only).
+
+    For a torch tensor the call checks what the C ABI cannot: that it lives on
+    the handle's GPU (``device``), is contiguous, has the sample dtype the handle
+    was built for (``dtype``, a numpy dtype) and holds at least ``count``
+    elements.  A raw int pointer is passed through unchecked (the caller vouches
+    for it, as a Rust caller of the C ABI does)."""
     if isinstance(t, int):
         return t
+    if not getattr(t, "is_cuda", False):
+        raise ValueError(f"{what}: expected a device (HIP) tensor")
+    if device is not None and t.device.index is not None and t.device.index != device:
+        raise ValueError(f"{what}: tensor on device {t.device.index}, handle on device {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+    if dtype is not None:
+        want = _torch_dtype(dtype)
+        if t.dtype != want:
+            raise ValueError(f"{what}: dtype {t.dtype}, handle expects {want}")
+    if count is not None and t.numel() < count:
+        raise ValueError(f"{what}: {t.numel()} elements, the call needs {count}")
     return int(t.data_ptr())
+
+
+def _torch_dtype(np_dtype):
+    import torch
+    return {np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64,
+            np.dtype(np.complex64): torch.complex64, np.dtype(np.complex128): torch.complex128}[np.dtype(np_dtype)]
 
 
 HIP_STREAM_LEGACY = 1  # hipStreamLegacy: the legacy null stream (torch's default stream)

@@ -26,6 +26,7 @@ class Channelizer:
                                          device))
         self._h = h
         self.M = channels
+        self.device = device
         self.streams = 1
         if streams != 1:
             self.set_streams(streams)
@@ -55,8 +56,9 @@ class Channelizer:
 
     def execute_block_device(self, d_in, n: int, d_out, stream=None) -> int:
         fr = C.c_size_t(0)
-        L.check(L.lib().sdsp_chan_execute_block_device(self._h, L.device_ptr(d_in), n, L.device_ptr(d_out),
-                                                        C.byref(fr), L.stream_handle(stream)))
+        pin = L.device_ptr(d_in, self.sample_dtype, self.streams * n, self.device, "input")
+        pout = L.device_ptr(d_out, self.sample_dtype, self.streams * n, self.device, "output")
+        L.check(L.lib().sdsp_chan_execute_block_device(self._h, pin, n, pout, C.byref(fr), L.stream_handle(stream)))
         return fr.value
 
     def synchronize(self):

@@ -92,28 +92,22 @@ struct sdsp_fir {
     DevBuf d_hist[2];                  // [channels][L-1] oldest first
     int cur = 0;
     size_t ci = 0;                     // DecimatingFIRFilter::current_item (decim.rs:7)
-    int algo = SDSP_ALGO_AUTO;
+    int algo = SDSP_ALGO_EXACT;        // reference-order kernel unless the caller opts in (sdsp.h)
     hipStream_t stream = nullptr;
+    mutable StreamFence fence;         // last stream an execute call was queued on
     DevBuf stage_in, stage_out;
     // overlap-save plan
     bool ols_ok = false;
-    bool ols_wide = true, ols_interleave = true;
-    int ols_depth2 = 2;  // SDSP_TUNE_OLS_SCHEDULE
-    bool ols_xcd = true;  // SDSP_TUNE_OLS_XCD_ORDER
-    int ols_nomem = 0;
-    int ols_nt = 0;
-    int ols_occ = 0;  // kernel variant (sdsp_fir_set_tuning)
+    int ols_kernel = kOlsOneShot;  // SDSP_TUNE_OLS_KERNEL
     int decim_seg = 0;  // outputs per lane group of the polyphase decimator (0 = auto)
     OlsPlan ols{};
-    DevBuf d_H, d_tw1, d_tw2, d_H1k, d_tw1k, d_pkt;
-    bool ols_wave = false;  // wave-per-segment N = 1024 kernel (SDSP_TUNE_OLS_WAVE)
-    int ols_segs = 16;  // SDSP_TUNE_OLS_SEGS_PER_BLOCK
-    int ols_packed = 1;  // packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED): 0 off, 1..6 builds
+    DevBuf d_H, d_tw1, d_tw2, d_pkt, d_ostab;
 };
 
 namespace {
 
 int fir_alloc_state(sdsp_fir* h) {
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
     for (int i = 0; i < 2; ++i) {
         SDSP_TRY(h->d_hist[i].ensure(hb), "alloc history");
@@ -131,6 +125,7 @@ bool ols_applicable(const sdsp_fir* h) {
 
 // spectrum of g[i] = scale * h[L-1-i] in the lane layout of kern_fir_ols.hip
 int ols_build(sdsp_fir* h) {
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const int N = kOlsN;
     const size_t L = h->L;
     const int h2 = (int)((L - 1 + 255) / 256);
@@ -195,43 +190,40 @@ int ols_build(sdsp_fir* h) {
     SDSP_TRY(h->d_pkt.ensure(pkt.size() * 4), "alloc packed tables");
     SDSP_TRY(hipMemcpyAsync(h->d_pkt.p, pkt.data(), pkt.size() * 4, hipMemcpyHostToDevice, h->stream),
              "copy packed tables");
-    // N = 1024 natural-order spectrum and twiddles for the wave-per-segment kernel (L - 1 <= 256)
-    int hr1k = 0;
-    if (L - 1 <= 256) {
-        hr1k = (int)((L - 1 + 63) / 64);
-        if (hr1k < 1) hr1k = 1;
-        std::vector<float> H1(2 * 1024), T1(2 * 1024);
-        const double w1 = -2.0 * M_PI / 1024.0;
-        for (int k = 0; k < 1024; ++k) {
-            double re = 0.0, im = 0.0;
-            for (size_t i = 0; i < L; ++i) {
-                const long long ph = ((long long)i * k) % 1024;
-                const double c = std::cos(w1 * (double)ph), sn = std::sin(w1 * (double)ph);
-                re += g[i].re * c - g[i].im * sn;
-                im += g[i].re * sn + g[i].im * c;
-            }
-            H1[2 * k] = (float)(re / 1024.0);
-            H1[2 * k + 1] = (float)(im / 1024.0);
-            T1[2 * k] = (float)std::cos(w1 * k);
-            T1[2 * k + 1] = (float)std::sin(w1 * k);
-        }
-        SDSP_TRY(h->d_H1k.ensure(H1.size() * 4), "alloc H1k");
-        SDSP_TRY(h->d_tw1k.ensure(T1.size() * 4), "alloc tw1k");
-        SDSP_TRY(hipMemcpyAsync(h->d_H1k.p, H1.data(), H1.size() * 4, hipMemcpyHostToDevice, h->stream), "copy H1k");
-        SDSP_TRY(hipMemcpyAsync(h->d_tw1k.p, T1.data(), T1.size() * 4, hipMemcpyHostToDevice, h->stream),
-                 "copy tw1k");
+    // one-shot kernel: per column c the twiddle bases C_b = W4096^(b c), D_a = W4096^(4 a c)
+    // (b, a = 1..3) as float4 [q][c] = (C1 C2 | C3 D1 | D2 D3), then the W256 rows
+    // float4 [r][p] = (W256^(r 2p), W256^(r (2p + 1)))
+    std::vector<float> os(4 * (768 + 128));
+    auto put = [&](size_t f4, int half, long long m, int nn) {
+        const double ang = -2.0 * M_PI * (double)(m % nn) / nn;
+        os[4 * f4 + 2 * half] = (float)std::cos(ang);
+        os[4 * f4 + 2 * half + 1] = (float)std::sin(ang);
+    };
+    for (int c = 0; c < 256; ++c) {
+        put(c, 0, c, 4096);
+        put(c, 1, 2LL * c, 4096);
+        put(256 + c, 0, 3LL * c, 4096);
+        put(256 + c, 1, 4LL * c, 4096);
+        put(512 + c, 0, 8LL * c, 4096);
+        put(512 + c, 1, 12LL * c, 4096);
     }
+    for (int r = 0; r < 16; ++r)
+        for (int p = 0; p < 8; ++p) {
+            put(768 + r * 8 + p, 0, (long long)r * 2 * p, 256);
+            put(768 + r * 8 + p, 1, (long long)r * (2 * p + 1), 256);
+        }
+    SDSP_TRY(h->d_ostab.ensure(os.size() * 4), "alloc one-shot tables");
+    SDSP_TRY(hipMemcpyAsync(h->d_ostab.p, os.data(), os.size() * 4, hipMemcpyHostToDevice, h->stream),
+             "copy one-shot tables");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
-    h->ols = OlsPlan{h->d_H.p, h->d_tw1.p, h->d_tw2.p, h2, h->ols_wide, h->ols_interleave, h->ols_depth2, h->ols_nomem, h->ols_occ};
-    h->ols.nt = h->ols_nt;
-    h->ols.d_H1k = hr1k ? h->d_H1k.p : nullptr;
-    h->ols.d_tw1k = hr1k ? h->d_tw1k.p : nullptr;
-    h->ols.halo_rows_1k = hr1k;
-    h->ols.wave = h->ols_wave && hr1k > 0;
-    h->ols.packed = h->ols_packed;
-    h->ols.segs_per_block = h->ols_segs;
-    h->ols.xcd = h->ols_xcd;
+    h->ols = OlsPlan{};
+    h->ols.d_H = h->d_H.p;
+    h->ols.d_tw1 = h->d_tw1.p;
+    h->ols.d_tw2 = h->d_tw2.p;
+    h->ols.halo_rows = h2;
+    h->ols.kernel = h->ols_kernel;
     h->ols.d_pkt = h->d_pkt.p;
+    h->ols.d_ostab = h->d_ostab.p;
     h->ols_ok = true;
     return SDSP_OK;
 }
@@ -340,9 +332,8 @@ void sdsp_fir_destroy(sdsp_fir* h) {
         h->d_H.release();
         h->d_tw1.release();
         h->d_tw2.release();
-        h->d_H1k.release();
-        h->d_tw1k.release();
         h->d_pkt.release();
+        h->d_ostab.release();
     }
     delete h;
 }
@@ -369,33 +360,19 @@ int sdsp_fir_get_algo(const sdsp_fir* h) { return h ? h->algo : -1; }
 int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     switch (key) {
-        // retired overlap-save variants (measured slower): only their default is accepted
-        case SDSP_TUNE_OLS_WIDE: h->ols_wide = value != 0; break;  // packed kernel only
-        case SDSP_TUNE_OLS_SCHEDULE:  // packed kernel, 16-byte rows, h2 = 1
-            if (value < 0 || value > 10) return SDSP_E_INVALID_ARGUMENT;
-            h->ols_depth2 = value;
-            break;
-        case SDSP_TUNE_OLS_XCD_ORDER: h->ols_xcd = value != 0; break;
-        case SDSP_TUNE_OLS_INTERLEAVE: h->ols_interleave = value != 0; break;
-        case SDSP_TUNE_OLS_NONTEMPORAL: h->ols_nt = value & 7; break;
-        case SDSP_TUNE_OLS_WAVE: h->ols_wave = value != 0; break;
-        case SDSP_TUNE_OLS_SEGS_PER_BLOCK: h->ols_segs = value >= -1 ? value : 0; break;  // -1: XCD-local interleave
-        case SDSP_TUNE_OLS_PACKED: h->ols_packed = (value >= 0 && value <= 6) ? value : 0; break;
-        case SDSP_TUNE_OLS_ABLATE_NOMEM: h->ols_nomem = (value >= 0 && value <= 10) ? value : 0; break;
-        case SDSP_TUNE_DECIM_SEG: h->decim_seg = value > 0 ? value : 0; break;
-        default: return SDSP_E_INVALID_ARGUMENT;
+        case SDSP_TUNE_OLS_KERNEL:  // every value computes the full output (performance only)
+            if (value < kOlsOneShot || value > kOlsScalar) return SDSP_E_INVALID_ARGUMENT;
+            h->ols_kernel = value;
+            h->ols.kernel = value;
+            return SDSP_OK;
+        case SDSP_TUNE_DECIM_SEG:
+            if (value < 0) return SDSP_E_INVALID_ARGUMENT;
+            h->decim_seg = value;
+            return SDSP_OK;
+        default:
+            set_error("unknown or retired tuning key");
+            return SDSP_E_INVALID_ARGUMENT;
     }
-    h->ols.wide = h->ols_wide;
-    h->ols.interleave = h->ols_interleave;
-    h->ols.depth2 = h->ols_depth2;
-    h->ols.xcd = h->ols_xcd;
-    h->ols.nomem = h->ols_nomem;
-    h->ols.nt = h->ols_nt;
-    h->ols.occ = h->ols_occ;
-    h->ols.wave = h->ols_wave && h->ols.halo_rows_1k > 0;
-    h->ols.packed = h->ols_packed;
-    h->ols.segs_per_block = h->ols_segs;
-    return SDSP_OK;
 }
 
 int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out) {
@@ -409,7 +386,10 @@ int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out) {
         st = sdsp_fir_set_channels(c, h->channels);
         if (st) return st;
     }
+    c->ols_kernel = h->ols_kernel;
+    c->decim_seg = h->decim_seg;
     const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     if (hb) SDSP_TRY(hipMemcpy(c->d_hist[0].p, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToDevice), "clone state");
     c->cur = 0;
@@ -419,6 +399,8 @@ int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out) {
 
 int sdsp_fir_set_scale(sdsp_fir* h, const void* scale) {
     if (!h || !scale) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");  // the next run rebuilds tables a queued kernel may read
     std::memcpy(h->scale.data(), scale, h->scale.size());
     h->ols_ok = false;
     return SDSP_OK;
@@ -454,6 +436,11 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
     const size_t nout = sdsp_fir_output_count(h, n);
     if (n_out) *n_out = nout;
     if (n == 0) return SDSP_OK;
+    const size_t sb = sample_bytes(h->dtype);
+    if (ranges_overlap(d_in, h->channels * n * sb, d_out, h->channels * nout * sb)) {
+        set_error("input and output blocks overlap (in-place filtering is not supported)");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
     const void* hist = h->d_hist[h->cur].p;
     if (h->M == 1) {
         const int algo = fir_resolve_algo(h, n);
@@ -480,12 +467,14 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
     SDSP_TRY(launch_hist_update(h->dtype, d_in, hist, h->d_hist[h->cur ^ 1].p, n, (int)h->L - 1, h->channels, s),
              "history update");
     h->cur ^= 1;
+    if (s != h->stream) SDSP_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 
 int sdsp_fir_execute_block(sdsp_fir* h, const void* in, size_t n, void* out, size_t* n_out) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const size_t sb = sample_bytes(h->dtype);
     const size_t nout = sdsp_fir_output_count(h, n);
     if (n_out) *n_out = nout;
@@ -511,6 +500,7 @@ int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (n == 0) return SDSP_OK;
     DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const size_t sb = sample_bytes(h->dtype);
     SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
     SDSP_TRY(hipMemcpyAsync(h->stage_in.p, samples, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
@@ -537,6 +527,7 @@ int sdsp_fir_get_state(const sdsp_fir* h, void* hist, size_t* phase) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuard g(h->device);
     const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     if (hb && hist) SDSP_TRY(hipMemcpy(hist, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToHost), "get state");
     if (phase) *phase = h->ci;
@@ -547,6 +538,7 @@ int sdsp_fir_set_state(sdsp_fir* h, const void* hist, size_t phase) {
     if (!h || phase >= h->M) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuard g(h->device);
     const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     if (hb && hist) SDSP_TRY(hipMemcpy(h->d_hist[h->cur].p, hist, hb, hipMemcpyHostToDevice), "set state");
     h->ci = phase;

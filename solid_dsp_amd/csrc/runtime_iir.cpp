@@ -100,7 +100,7 @@ struct sdsp_iir {
     std::vector<Group> groups;
     DevBuf d_coefs, d_state[2], d_tmp[2];
     int cur = 0;
-    int algo = SDSP_ALGO_AUTO;
+    int algo = SDSP_ALGO_EXACT;  // reference-order recurrence unless the caller opts in (sdsp.h)
     int wscan = 1;  // 0: block scan; 1-4: wave-scan variant 0-3 (kern_iir_wscan.hip; sdsp_iir_set_tuning)
     hipStream_t stream = nullptr;
     DevBuf stage_in, stage_out;

@@ -75,4 +75,40 @@ struct DevBuf {
     }
 };
 
+// Completion marker of the last work a handle queued on a caller's stream.
+// *_execute_block_device may run on any stream; host-side state operations
+// (reset, set_state / get_state, clone, table rebuilds after set_scale) first
+// wait for that work, so a kernel still reading the delay line or the tables is
+// never raced by a host copy on the handle's own stream.
+struct StreamFence {
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    StreamFence() = default;
+    StreamFence(const StreamFence&) = delete;
+    StreamFence& operator=(const StreamFence&) = delete;
+    ~StreamFence() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    hipError_t record(hipStream_t s) {
+        if (!ev) {
+            hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        pending = true;
+        return hipEventRecord(ev, s);
+    }
+    hipError_t wait() {
+        if (!pending) return hipSuccess;
+        pending = false;
+        return hipEventSynchronize(ev);
+    }
+};
+
+// [a, a + na) and [b, b + nb) overlap (byte ranges)
+inline bool ranges_overlap(const void* a, size_t na, const void* b, size_t nb) {
+    if (!na || !nb) return false;
+    const auto pa = reinterpret_cast<uintptr_t>(a), pb = reinterpret_cast<uintptr_t>(b);
+    return pa < pb + nb && pb < pa + na;
+}
+
 }  // namespace sdsp

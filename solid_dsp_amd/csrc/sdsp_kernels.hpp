@@ -28,46 +28,31 @@ hipError_t launch_hist_update(int dtype, const void* x, const void* old_hist, vo
                               size_t channels, hipStream_t s);
 
 // overlap-save (N = 4096) for 32-bit complex samples
+constexpr int kOlsOneShot = 0;     // interior segments: one-shot XCD-ordered kernel (kern_fir_ols_os.hip)
+constexpr int kOlsPersistent = 1;  // persistent packed kernel, kOlsSegsPerBlock segments per workgroup
+constexpr int kOlsScalar = 2;      // scalar persistent kernel for every segment (kern_fir_ols.hip)
+constexpr int kOlsSegsPerBlock = 16;
 struct OlsPlan {
     void* d_H;    // [256][16] c32: H[k0 + 16 k1 + 256 k2] / N * scale, row t = 16 k0 + k1
     void* d_tw1;  // [256][16] c32: W4096^(t*k)
     void* d_tw2;  // [16][16]  c32: W256^(a*b)
     int halo_rows;  // h2: halo = 256*h2 >= L-1
-    bool wide;        // 16-byte lane-pair global loads/stores
-    bool interleave;  // segment order across the persistent grid
-    int depth2;       // packed kernel (16-byte rows, h2 = 1) HBM issue schedule: 0 default, 1 two segments of
-                      // loads in flight, 2..6 one segment with the SCH tables 1..5 of kern_fir_ols_pk.hip
-    int nomem;        // profiling ablation (outputs invalid): 1 no HBM traffic, 2 no loads, 3 no stores,
-                      // 4 no HBM + no barriers; packed kernel: 5 no HBM + no barriers, 6 also no LDS,
-                      // 7 HBM traffic only
-    int occ;          // retired (0)
-    int nt = 0;       // nontemporal: bit 0 loads, bit 1 stores
-    // wave-per-segment N = 1024 kernel (L - 1 <= 256)
-    void* d_H1k = nullptr;   // [1024] c32: natural-order spectrum / 1024 * scale
-    void* d_tw1k = nullptr;  // [1024] c32: W1024^m
-    int halo_rows_1k = 0;    // HR: 64 HR >= L - 1
-    bool wave = false;
-    int packed = 0;  // packed-FP32 interior kernel (kern_fir_ols_pk.hip): odd = asm table products, even = compiler-
-                     // visible; 1-2 default scheduler, 3-4 max-ilp, 5-6 iterative-ilp
-    int segs_per_block = 0;  // packed kernel: 0 persistent interleaved grid, > 0 consecutive segments per workgroup
-    void* d_pkt = nullptr;   // packed kernel tables, k-pair major (runtime.cpp ols_build)
-    bool xcd = true;         // packed kernel, segs_per_block > 0: workgroup b % 8 (its XCD) takes a contiguous 1/8 of the chunks
+    int kernel = kOlsOneShot;
+    void* d_pkt = nullptr;    // k-pair major tables: [0, 2048) float4 spectrum rows, [2048, 4096) W4096 rows,
+                              // [4096, 4224) W256 rows (runtime.cpp ols_build)
+    void* d_ostab = nullptr;  // one-shot kernel: [3][256] float4 twiddle bases per column
+                              // (C1 C2 | C3 D1 | D2 D3), then [16][8] float4 W256 rows
 };
 constexpr int kOlsN = 4096;
 hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
                           size_t channels, int num_cus, hipStream_t s);
 // interior segments [lo, hi) of a call: whole input window and all outputs inside the stream
 void ols_interior_range(long long n, int h2, long long* lo, long long* hi);
-// packed interior kernel, one build per scheduling strategy (kern_fir_ols_pk.hip)
-#define SDSP_DECL_OLS_PK(NS)                                                                                      \
-    namespace NS {                                                                                                \
-    hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, int num_cus, \
-                                 hipStream_t s, long long lo, long long hi, int ablate);                          \
-    }
-SDSP_DECL_OLS_PK(pk_default)
-SDSP_DECL_OLS_PK(pk_ilp)
-SDSP_DECL_OLS_PK(pk_iilp)
-#undef SDSP_DECL_OLS_PK
+// interior-segment kernels (16-byte rows)
+hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
+                             long long lo, long long hi);
+hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
+                             long long lo, long long hi);
 
 // polyphase filterbank / interpolator: out[j*M + p] = sum_{i<K} cb[p*K + i] * ext(j - i)
 struct PfbArgs {

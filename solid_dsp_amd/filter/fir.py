@@ -35,7 +35,7 @@ class _FirBase:
     _decim = False
 
     def __init__(self, coefs, scale, decimation=1, sample_dtype=None, coef_dtype=None, device=0, channels=1,
-                 algo=L.ALGO_AUTO):
+                 algo=None):
         c = _coef_array(coefs, coef_dtype)
         if sample_dtype is None:
             sample_dtype = _default_sample(c.dtype)
@@ -50,20 +50,22 @@ class _FirBase:
         else:
             L.check(lib.sdsp_fir_create(C.byref(h), self.dtype, L.ptr(c), len(c), L.ptr(s), device))
         self._h = h
+        self.device = device
         self.channels = 1
         if channels != 1:
             self.set_channels(channels)
-        if algo != L.ALGO_AUTO:
+        if algo is not None:  # default: the handle's ALGO_EXACT (bit-identical to the reference)
             self.set_algo(algo)
 
     @classmethod
-    def _wrap(cls, handle, dtype, channels):
+    def _wrap(cls, handle, dtype, channels, device=0):
         obj = cls.__new__(cls)
         obj._h = handle
         obj.dtype = dtype
         obj.coef_dtype = L.COEF_DTYPE[dtype]
         obj.sample_dtype = L.SAMPLE_DTYPE[dtype]
         obj.channels = channels
+        obj.device = device
         return obj
 
     def __del__(self):
@@ -107,7 +109,7 @@ class _FirBase:
     def clone(self):
         h = C.c_void_p()
         L.check(L.lib().sdsp_fir_clone(self._h, C.byref(h)))
-        return type(self)._wrap(h, self.dtype, self.channels)
+        return type(self)._wrap(h, self.dtype, self.channels, self.device)
 
     __copy__ = clone
 
@@ -151,10 +153,12 @@ class _FirBase:
         return y
 
     def execute_block_device(self, d_in, n: int, d_out, stream=None) -> int:
-        """Device-resident execute_block: d_in/d_out are torch tensors or raw device pointers."""
+        """Device-resident execute_block: d_in/d_out are torch tensors or raw device pointers
+        (channel-major, n samples per channel in, output_count(n) per channel out)."""
         got = C.c_size_t(0)
-        L.check(L.lib().sdsp_fir_execute_block_device(self._h, L.device_ptr(d_in), n, L.device_ptr(d_out),
-                                                       C.byref(got), L.stream_handle(stream)))
+        pin = L.device_ptr(d_in, self.sample_dtype, self.channels * n, self.device, "input")
+        pout = L.device_ptr(d_out, self.sample_dtype, self.channels * self.output_count(n), self.device, "output")
+        L.check(L.lib().sdsp_fir_execute_block_device(self._h, pin, n, pout, C.byref(got), L.stream_handle(stream)))
         return got.value
 
     def synchronize(self):
@@ -178,7 +182,7 @@ class FIRFilter(_FirBase):
     """
 
     def __init__(self, coefs, scale=1.0, sample_dtype=None, coef_dtype=None, device=0, channels=1,
-                 algo=L.ALGO_AUTO):
+                 algo=None):
         super().__init__(coefs, scale, 1, sample_dtype, coef_dtype, device, channels, algo)
 
     @classmethod
@@ -192,7 +196,7 @@ class DecimatingFIRFilter(_FirBase):
     _decim = True
 
     def __init__(self, coefs, scale=1.0, decimation=1, sample_dtype=None, coef_dtype=None, device=0,
-                 channels=1, algo=L.ALGO_AUTO):
+                 channels=1, algo=None):
         super().__init__(coefs, scale, decimation, sample_dtype, coef_dtype, device, channels, algo)
 
     @classmethod
@@ -228,6 +232,7 @@ class PolyPhaseFilterBank:
         else:
             L.check(L.lib().sdsp_interp_create(C.byref(h), self.dtype, L.ptr(c), len(c), _interp, device))
         self._h = h
+        self.device = device
 
     @classmethod
     def new(cls, coefs, filters, scale, **kw):
@@ -296,8 +301,9 @@ class PolyPhaseFilterBank:
         return y
 
     def execute_block_device(self, d_in, n: int, d_out, stream=None):
-        L.check(L.lib().sdsp_pfb_execute_block_device(self._h, L.device_ptr(d_in), n, L.device_ptr(d_out),
-                                                       L.stream_handle(stream)))
+        pin = L.device_ptr(d_in, self.sample_dtype, n, self.device, "input")
+        pout = L.device_ptr(d_out, self.sample_dtype, n * self.len(), self.device, "output")
+        L.check(L.lib().sdsp_pfb_execute_block_device(self._h, pin, n, pout, L.stream_handle(stream)))
         return n * self.len()
 
     def synchronize(self):

@@ -29,7 +29,7 @@ class _IirBase:
     _mode = 0
 
     def __init__(self, feed_forward, feed_back, iirtype=IIRFilterType.SecondOrder, factor=1, sample_dtype=None,
-                 coef_dtype=None, device=0, channels=1, algo=L.ALGO_AUTO):
+                 coef_dtype=None, device=0, channels=1, algo=None):
         ff = np.asarray(feed_forward)
         cdt = np.dtype(coef_dtype) if coef_dtype is not None else (
             ff.dtype if ff.dtype in (np.float32, np.float64) else np.dtype(np.float64))
@@ -53,10 +53,11 @@ class _IirBase:
             L.check(lib.sdsp_iir_interp_create(*args, factor, device))
         self._h = h
         self._factor = factor
+        self.device = device
         self.channels = 1
         if channels != 1:
             self.set_channels(channels)
-        if algo != L.ALGO_AUTO:
+        if algo is not None:  # default: the handle's ALGO_EXACT (bit-identical to the reference)
             self.set_algo(algo)
 
     def __del__(self):
@@ -153,8 +154,9 @@ class _IirBase:
 
     def execute_block_device(self, d_in, n, d_out, stream=None) -> int:
         got = C.c_size_t(0)
-        L.check(L.lib().sdsp_iir_execute_block_device(self._h, L.device_ptr(d_in), n, L.device_ptr(d_out),
-                                                       C.byref(got), L.stream_handle(stream)))
+        pin = L.device_ptr(d_in, self.sample_dtype, self.channels * n, self.device, "input")
+        pout = L.device_ptr(d_out, self.sample_dtype, self.channels * self.output_count(n), self.device, "output")
+        L.check(L.lib().sdsp_iir_execute_block_device(self._h, pin, n, pout, C.byref(got), L.stream_handle(stream)))
         return got.value
 
     def synchronize(self):

@@ -131,74 +131,116 @@ def test_fir_fft_tolerance(dt, cdt, L):
     assert np.abs(y - ref).max() <= bound
 
 
-@pytest.mark.parametrize("dt,cdt", [(O.RC32, F32), (O.CC32, C64)])
-@pytest.mark.parametrize("L", [2, 64, 200, 256, 257])
-def test_fir_fft_wave_kernel_tolerance(dt, cdt, L):
-    # wave-per-segment N=1024 overlap-save (SDSP_TUNE_OLS_WAVE = 11): ragged calls, vs f64 restatement
+OLS_ONESHOT, OLS_PERSISTENT, OLS_SCALAR = 0, 1, 2
+TUNE_OLS_KERNEL = 14
+
+
+@pytest.mark.parametrize("L", [2, 64, 256, 257, 700, 1025, 2000, 3841])
+@pytest.mark.parametrize("ch", [1, 2, 3])
+def test_fir_fft_oneshot_kernel_tolerance(L, ch):
+    # default interior kernel (one-shot, XCD-ordered) + boundary kernel, ragged calls that
+    # cover all-boundary calls (n < one window), history carry and both edges, every halo
+    # size h2 = 1..15; ch = 3 with odd n falls back to the scalar kernel (8-byte rows)
     h = _f32_taps(L, 0.1)
-    if cdt == C64:
-        h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
-    x = O.synth(20250226, 2, 0, 400000, complex_=True)
-    f = FIRFilter(h, cdt(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
-    assert sd.lib().sdsp_fir_set_tuning(f._h, 11, 1) == 0
-    cuts = [0, 1, 1000, 70001, 300007, 400000]
-    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(cuts[:-1], cuts[1:])])
-    ref = O.fir(O.CC64, h.astype(C128), 0.2 + 0j).execute_block(x.astype(C128))
-    assert rel_rms(y, ref) <= 1e-6
-    bound = 1e-6 * np.abs(h).sum() * 0.2 * np.abs(x).max()
-    assert np.abs(y - ref).max() <= bound
+    h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
+    x = O.synth(20250229, 6, 0, 300000 * ch, complex_=True).reshape(ch, -1) if ch > 1 else \
+        O.synth(20250229, 6, 0, 300000, complex_=True)
+    f = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
+    cuts = [0, 1, 3000, 7001, 70002, 207714, 300000]
+    y = np.concatenate([f.execute_block(x[..., a:b]) for a, b in zip(cuts[:-1], cuts[1:])], axis=-1)
+    for c in range(ch):
+        xc = x[c] if ch > 1 else x
+        yc = y[c] if ch > 1 else y
+        ref = O.fir(O.CC64, h.astype(C128), 0.2 + 0j).execute_block(xc.astype(C128))
+        assert rel_rms(yc, ref) <= 1e-6, (L, ch, c)
+        bound = 1e-6 * np.abs(h).sum() * 0.2 * np.abs(xc).max()
+        assert np.abs(yc - ref).max() <= bound, (L, ch, c)
 
 
-@pytest.mark.parametrize("L,pk,per,wide", [(L, 1, 0, 0) for L in (2, 64, 256, 513, 1000)] +
-                         [(L, pk, 0, 0) for L in (257, 1025) for pk in range(1, 7)] +
-                         [(257, 5, per, 0) for per in (1, 3, 16)] +
-                         [(L, pk, 0, 1) for L in (64, 513, 700, 1025) for pk in (5, 6)] +
-                         [(257, 5, 16, 1), (700, 1, 3, 1)])
+@pytest.mark.parametrize("L", [2, 64, 257, 513, 1025])
 @pytest.mark.parametrize("ch", [1, 3])
-def test_fir_fft_packed_kernel_bit_identical(L, pk, per, wide, ch):
-    # packed-FP32 interior kernel (SDSP_TUNE_OLS_PACKED = 12, builds 1..6: table products as asm
-    # or compiler-visible, three scheduling strategies) + boundary-segment kernel vs the scalar
-    # overlap-save kernel: the same IEEE operations per component, so identical bits; ragged
-    # calls cover all-boundary calls (n < one window), history and both edges
+def test_fir_fft_persistent_kernel_bit_identical(L, ch):
+    # persistent packed interior kernel (SDSP_TUNE_OLS_KERNEL = 1) + boundary kernel vs the
+    # scalar overlap-save kernel (= 2): the same IEEE operations per component, so identical bits
     h = _f32_taps(L, 0.1)
     h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
     x = O.synth(20250227, 4, 0, 300000 * ch, complex_=True).reshape(ch, -1) if ch > 1 else \
         O.synth(20250227, 4, 0, 300000, complex_=True)
     a = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
     b = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
-    assert sd.lib().sdsp_fir_set_tuning(a._h, 12, pk) == 0
-    assert sd.lib().sdsp_fir_set_tuning(a._h, 13, per) == 0
-    assert sd.lib().sdsp_fir_set_tuning(a._h, 1, wide) == 0  # 16-byte accesses (even n or one channel)
-    assert sd.lib().sdsp_fir_set_tuning(b._h, 12, 0) == 0
-    cuts = [0, 1, 3000, 7001, 70001, 207714, 300000]
+    assert sd.lib().sdsp_fir_set_tuning(a._h, TUNE_OLS_KERNEL, OLS_PERSISTENT) == 0
+    assert sd.lib().sdsp_fir_set_tuning(b._h, TUNE_OLS_KERNEL, OLS_SCALAR) == 0
+    cuts = [0, 1, 3000, 7002, 70002, 207714, 300000]
     for lo, hi in zip(cuts[:-1], cuts[1:]):
         xa = x[..., lo:hi]
-        assert bits_equal(a.execute_block(xa), b.execute_block(xa)), (L, pk, per, wide, ch, lo, hi)
-    ref = O.fir(O.CC64, h.astype(C128), 0.2 + 0j).execute_block((x[-1] if ch > 1 else x).astype(C128))
-    a.reset()
-    y = a.execute_block(x)
-    assert rel_rms(y[-1] if ch > 1 else y, ref) <= 1e-6
+        assert bits_equal(a.execute_block(xa), b.execute_block(xa)), (L, ch, lo, hi)
 
 
-@pytest.mark.parametrize("sched,xcd,per", [(v, 1, 16) for v in range(11)] + [(2, 0, 16), (2, 1, 3), (10, 1, 1)])
-@pytest.mark.parametrize("ch", [1, 2])
-def test_fir_fft_packed_schedules_bit_identical(sched, xcd, per, ch):
-    # HBM issue schedules (SDSP_TUNE_OLS_SCHEDULE = 3: burst / two segments ahead / spread over
-    # the phases) and the XCD-contiguous chunk order (SDSP_TUNE_OLS_XCD_ORDER = 5) only move
-    # loads and stores: bits equal the scalar overlap-save kernel across ragged calls
+def test_fir_tuning_rejects_retired_and_bad_keys():
+    # no tuning value may leave the output unwritten: retired ablation keys are refused
+    f = FIRFilter(_f32_taps(64, 0.1), F32(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    for key in (1, 2, 3, 4, 5, 10, 11, 12, 13, 99):
+        assert sd.lib().sdsp_fir_set_tuning(f._h, key, 1) == 90, key
+    assert sd.lib().sdsp_fir_set_tuning(f._h, TUNE_OLS_KERNEL, 3) == 90
+    for v in (OLS_ONESHOT, OLS_PERSISTENT, OLS_SCALAR):
+        assert sd.lib().sdsp_fir_set_tuning(f._h, TUNE_OLS_KERNEL, v) == 0
+
+
+def test_fir_default_algo_is_exact_for_large_blocks():
+    # a handle built with no algo is bit-identical to the reference restatement at any block
+    # size (the overlap-save and scan kernels are opt-in)
     h = _f32_taps(256, 0.1)
-    x = O.synth(20250228, 5, 0, 400000 * ch, complex_=True)
-    x = x.reshape(ch, -1) if ch > 1 else x
-    a = FIRFilter(h, F32(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
-    b = FIRFilter(h, F32(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
-    assert sd.lib().sdsp_fir_set_tuning(a._h, 3, sched) == 0
-    assert sd.lib().sdsp_fir_set_tuning(a._h, 5, xcd) == 0
-    assert sd.lib().sdsp_fir_set_tuning(a._h, 13, per) == 0
-    assert sd.lib().sdsp_fir_set_tuning(b._h, 12, 0) == 0
-    cuts = [0, 5, 4000, 123457, 400000]
-    for lo, hi in zip(cuts[:-1], cuts[1:]):
-        xa = x[..., lo:hi]
-        assert bits_equal(a.execute_block(xa), b.execute_block(xa)), (sched, xcd, per, ch, lo, hi)
+    x = O.synth(11, 1, 0, 1 << 17, complex_=True)
+    f = FIRFilter(h, F32(0.2), sample_dtype=C64)
+    assert bits_equal(f.execute_block(x), O.fir(O.RC32, h, F32(0.2)).execute_block(x))
+
+
+def test_fir_rejects_in_place_and_bad_device_buffers():
+    import torch
+    h = _f32_taps(64, 0.1)
+    n = 1 << 16
+    f = FIRFilter(h, F32(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    buf = to_dev(O.synth(3, 0, 0, 2 * n, complex_=True))
+    with pytest.raises(sd.SdspError) as e:  # in place
+        f.execute_block_device(buf, n, buf)
+    assert e.value.code == 90
+    with pytest.raises(sd.SdspError):  # partial overlap
+        f.execute_block_device(buf, n, buf[n // 2:])
+    ok = empty_dev(n, C64)
+    with pytest.raises(ValueError):  # undersized output
+        f.execute_block_device(buf[:n], n, ok[: n - 1])
+    with pytest.raises(ValueError):  # wrong dtype
+        f.execute_block_device(buf[:n].view(torch.float32), n, ok)
+    with pytest.raises(ValueError):  # host tensor
+        f.execute_block_device(torch.zeros(n, dtype=torch.complex64), n, ok)
+    assert f.execute_block_device(buf[:n], n, ok) == n
+
+
+def test_fir_side_stream_set_scale_and_state_are_ordered():
+    # work queued on a caller stream must finish before set_scale's table rebuild,
+    # get_state, clone or reset touch the handle's device buffers
+    import torch
+    h = _f32_taps(256, 0.1)
+    n = 1 << 22
+    x = O.synth(5, 2, 0, n, complex_=True)
+    d_in = to_dev(x)
+    s = torch.cuda.Stream()
+    f = FIRFilter(h, F32(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    outs = [empty_dev(n, C64) for _ in range(2)]
+    with torch.cuda.stream(s):
+        f.execute_block_device(d_in, n, outs[0], s)
+        f.set_scale(F32(0.5))
+        f.execute_block_device(d_in, n, outs[1], s)
+        hist, _ = f.get_state()
+        g = f.clone()
+    torch.cuda.synchronize()
+    assert bits_equal(hist, x[-255:])
+    ref = FIRFilter(h, F32(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    r0 = ref.execute_block(x)
+    ref.set_scale(F32(0.5))
+    r1 = ref.execute_block(x)
+    assert bits_equal(to_host(outs[0]), r0) and bits_equal(to_host(outs[1]), r1)
+    assert bits_equal(g.execute_block(x[:1000]), ref.execute_block(x[:1000]))
 
 
 def test_fir_fft_matches_exact_kernel_across_calls():
