@@ -20,7 +20,12 @@ SURVEY §8f rows (build-defined cases, same parity + measurement fields):
 
 With N ranks each rank processes its own independent channel(s) (weak
 scaling, no collective in the timed region); RCCL is used afterwards only for
-the final gather, timed separately.  rank 0 prints one JSON line.
+the final gather of every rank's whole output to rank 0, timed separately
+(`gather`) and checked there against the f64 restatement.  rank 0 prints one
+JSON line.  `--gpus N` under torch.distributed.run must equal WORLD_SIZE;
+without a torchrun environment this script (never touching the GPU itself)
+spawns the N ranks.  `--dry-run` rehearses launch, timing and gather on the
+CPU over gloo.
 """
 import argparse
 import json
@@ -40,7 +45,8 @@ SEED = 20250226
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); outside torch.distributed.run this process spawns them itself")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5, 6, 7, 8, 9])
@@ -50,6 +56,9 @@ def parse():
                    help="bounded sample of the same workload timed on the host (oracle restatement)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--no-gather", action="store_true", help="skip the final RCCL gather of every rank's output")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU-only rehearsal of the rank launch, timing and gather over gloo (no GPU)")
     return p.parse_args()
 
 
@@ -70,9 +79,11 @@ def load_traffic(config, log2n, algo, kernel=""):
     return None
 
 
-def stream_copy_gbps(torch, sd, nbytes=4 << 30, reps=5):
+def stream_copy_gbps(torch, sd, nbytes=4 << 30, seconds=0.3):
     """Achievable HBM bandwidth on this box: one-shot 16-byte-per-lane device copy
-    (read + write bytes / time, median of `reps`), measured in the same run."""
+    (read + write bytes / time), repeated for ~`seconds` of device time; the
+    median of the second half of the repetitions (the first half lets the clocks
+    settle)."""
     a = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
     b = torch.empty_like(a)
     a.fill_(1.0)
@@ -80,7 +91,7 @@ def stream_copy_gbps(torch, sd, nbytes=4 << 30, reps=5):
     L = sd.lib()
     L.sdsp_bandwidth_copy_device(a.data_ptr(), b.data_ptr(), nbytes, st.cuda_stream)
     ts = []
-    for _ in range(reps):
+    while len(ts) < 8 or (sum(ts) < seconds * 1e3 and len(ts) < 400):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
         L.sdsp_bandwidth_copy_device(a.data_ptr(), b.data_ptr(), nbytes, st.cuda_stream)
@@ -89,7 +100,7 @@ def stream_copy_gbps(torch, sd, nbytes=4 << 30, reps=5):
         ts.append(e0.elapsed_time(e1))
     del a, b
     torch.cuda.empty_cache()
-    return 2.0 * nbytes / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e9
+    return 2.0 * nbytes / (float(np.median(ts[len(ts) // 2:])) * 1e-3) / 1e9
 
 
 def timed_cpu(run_chunk, label, samples, chunk, cores=1):
@@ -122,6 +133,7 @@ class Cfg2FIR:
     """256-tap crcf FIR, firdes_kaiser(256, 0.1, 80) taps rounded to f32, scale 0.2."""
     metric = "Msamples/sec 256-tap complex FIR @1/2/4/8 GPU; % HBM roofline"
     taps = 256
+    tol = 1e-6
 
     def __init__(self, args, rank, dev, torch, sd):
         from solid_dsp_amd import FIRFilter
@@ -166,6 +178,20 @@ class Cfg2FIR:
             worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
         return worst
 
+    def check_gathered(self, big, rng, width=4096):
+        """every rank's gathered output (channel = rank): two random windows each,
+        recomputed in f64 from that channel's synthetic inputs"""
+        import oracle_lib as O
+        worst, L = 0.0, self.taps
+        for r in range(big.shape[0]):
+            for _ in range(2):
+                s = int(rng.integers(L, self.n - width))
+                xs = O.synth(SEED, r, s - (L - 1), width + L - 1, complex_=True).astype(np.complex128)
+                ref = O.fir(O.RC64, self.h.astype(np.float64), 0.2).execute_block(xs)[L - 1:]
+                ys = big[r, s: s + width].cpu().numpy()
+                worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
+        return worst
+
     def cpu(self, samples):
         import oracle_lib as O
         x = O.synth(SEED, 0, 0, CPU_CHUNK, complex_=True).astype(np.complex128)
@@ -177,6 +203,7 @@ class Cfg2FIR:
 class Cfg3IIR:
     """4-section SOS cascade, scipy butter(8, 0.2), real f32 stream, block-parallel scan."""
     metric = "Msamples/sec 4-stage IIR biquad cascade (f32, 1 GiS); % HBM roofline"
+    tol = 1e-5
 
     def __init__(self, args, rank, dev, torch, sd):
         from solid_dsp_amd import IIRFilter, IIRFilterType
@@ -225,6 +252,7 @@ class Cfg3IIR:
 class Cfg4Decim:
     """M=32 decimator, firdes_kaiser(256, 1/64, 80) rounded to f32, scale 1/32, crcf."""
     metric = "Msamples/sec 32-branch polyphase decimator (M=32, 8 taps/branch); % HBM roofline"
+    tol = 1e-6
 
     def __init__(self, args, rank, dev, torch, sd):
         from solid_dsp_amd import DecimatingFIRFilter
@@ -265,6 +293,23 @@ class Cfg4Decim:
             ref = sliding_window_view(xs, 256)[::32][:width] @ h / 32.0
             ys = self.d_out[m: m + width].cpu().numpy()
             worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
+        return worst
+
+    def output(self):
+        return self.d_out[: self.n // 32]
+
+    def check_gathered(self, big, rng, width=4096):
+        """every rank's gathered decimated output (channel = rank), two random windows each"""
+        from numpy.lib.stride_tricks import sliding_window_view
+        import oracle_lib as O
+        h, worst = self.h.astype(np.float64), 0.0
+        for r in range(big.shape[0]):
+            for _ in range(2):
+                m = int(rng.integers(8, self.n // 32 - width))
+                xs = O.synth(SEED, r, 32 * m - 224, 32 * width + 224, complex_=True).astype(np.complex128)
+                ref = sliding_window_view(xs, 256)[::32][:width] @ h / 32.0
+                ys = big[r, m: m + width].cpu().numpy()
+                worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
         return worst
 
     def cpu(self, samples):
@@ -335,6 +380,7 @@ class Cfg1FIR:
     """cfg1 plumbing case: 63-tap real f32 FIR, firdes_kaiser(63, 0.2, 60), 2^20 samples,
     reference-order EXACT kernel (bit-identical to the f32 restatement)."""
     metric = "Msamples/sec 63-tap real-f32 FIR, 1 MiS (plumbing case)"
+    tol = 0
 
     def __init__(self, args, rank, dev, torch, sd):
         from solid_dsp_amd import FIRFilter
@@ -383,6 +429,7 @@ class Cfg6ACorr:
     """AutoCorrelator(window 64, delay 16), Complex<f32>, 2^29 samples: one read of x and
     one write of y per sample (src/filter/auto_correlator/mod.rs:181-191)."""
     metric = "Msamples/sec AutoCorrelator(64, 16) execute_block, c32; % HBM roofline"
+    tol = 0
 
     def __init__(self, args, rank, dev, torch, sd):
         self.W, self.D = 64, 16
@@ -477,6 +524,7 @@ class Cfg7NCO:
 class Cfg8FFT:
     """Batched 2^20-point forward FFT, Complex<f32>, 256 transforms per step (src/fft/mod.rs)."""
     metric = "Msamples/sec batched 2^20-point FFT, c32; % HBM roofline"
+    tol = 5e-6
 
     def __init__(self, args, rank, dev, torch, sd):
         from solid_dsp_amd import FFT, FFTDirection
@@ -528,6 +576,7 @@ class Cfg9AGC:
     """AGC bank: 2^18 independent AGC(bandwidth 0.02, squelch -30 dB) channels x 2^10
     Complex<f64> samples (src/auto_gain_control/mod.rs:214-285); one lane per channel."""
     metric = "Msamples/sec AGC execute_block, Complex<f64>, 2^18 channels; % HBM roofline"
+    tol = 1e-12
 
     def __init__(self, args, rank, dev, torch, sd):
         self.ch, self.n = 1 << 18, 1 << 10
@@ -595,13 +644,80 @@ CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 
 CPU_CHUNK = 1 << 22
 
 
-def main():
-    args = parse()
+def spawn_ranks(n):
+    """`--gpus N` outside torch.distributed.run: this parent never initialises the
+    GPU; it starts N child ranks of this same script (one per GPU) with
+    RANK / WORLD_SIZE / LOCAL_RANK and a 127.0.0.1 rendezvous, waits for all of
+    them, stops the rest when one fails, and returns the worst exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc, pending = 0, list(procs)
+    while pending:
+        for p in list(pending):
+            r = p.poll()
+            if r is None:
+                continue
+            pending.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 128 - r
+                for q in pending:
+                    q.terminate()
+        time.sleep(0.1)
+    return rc
+
+
+def dry_run(args, rank, world):
+    """CPU-only rehearsal of the N-rank harness over gloo (no GPU, no oracle):
+    every rank filters its own channel (numpy), the job time is the max over
+    ranks, and the whole output of every rank is gathered on rank 0 in small
+    chunks and checked there against a recomputation."""
     import torch
     import torch.distributed as dist
+    from solid_dsp_amd import parallel as P
+    if world > 1:
+        dist.init_process_group("gloo")
+    n, h = 1 << 14, np.hanning(64)
 
+    def channel(c):
+        x = np.random.default_rng([SEED, c]).standard_normal(2 * n).view(np.complex128)
+        return 0.2 * np.convolve(x, h)[:n]
+    t0 = time.perf_counter()
+    y = channel(rank)
+    wall = P.max_over_ranks(time.perf_counter() - t0)
+    ranks = P.gather_to_root(torch.tensor([rank], dtype=torch.int64), 0)
+    big = P.gather_full_to_root(torch.from_numpy(y.view(np.float64).copy()), 0, chunk_bytes=1 << 15)
+    if rank == 0:
+        ok = all(np.array_equal(big[r].numpy().view(np.complex128), channel(r)) for r in range(world))
+        print(json.dumps({"metric": "dry-run: rank launch + max-over-ranks timing + full gather (gloo, CPU)",
+                          "value": world * n / wall / 1e6, "unit": "Msamples/sec", "n_gpus": world,
+                          "ranks": [int(t.item()) for t in ranks], "gather_rows": int(big.shape[0]),
+                          "gather_ok": bool(ok), "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
     from solid_dsp_amd import parallel as P
     rank, world, local = P.world()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, rank, world)
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -614,6 +730,10 @@ def main():
     stream = torch.cuda.current_stream()
     w = WORKLOADS[args.config](args, rank, dev, torch, sd)
     torch.cuda.synchronize()
+    # achievable copy bandwidth of this box, measured before the warm-up: it also
+    # brings the device out of its idle clocks (~0.3 s of streaming) so the
+    # workload's own warm-up steps are not spent on the clock ramp
+    copy_gbps = stream_copy_gbps(torch, sd)
 
     for _ in range(args.warmup):
         w.step(stream)
@@ -636,17 +756,24 @@ def main():
     ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
     wall = P.max_over_ranks(wall, device="cuda")  # the job runs as long as its slowest rank
 
-    # final gather over RCCL (timed separately, not part of `value`): the first
-    # 2^20 outputs of every rank's channel to rank 0
-    gather_ms = None
-    if world > 1:
-        piece = w.d_out[: 1 << 20].contiguous()
+    # final gather over RCCL (timed separately, not part of `value`): every rank's
+    # whole output to rank 0, checked there against the f64 restatement
+    gather = None
+    if world > 1 and not args.no_gather:
+        piece = w.output() if hasattr(w, "output") else w.d_out
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter()
-        P.gather_to_root(piece, 0)
+        big = P.gather_full_to_root(piece, 0)
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
+        g_ms = (time.perf_counter() - tg) * 1e3
+        nbytes = world * piece.numel() * piece.element_size()
+        gather = {"ms": round(g_ms, 2), "bytes": nbytes, "GBps_into_root": round(nbytes / (g_ms * 1e-3) / 1e9, 1),
+                  "check": None}
+        if rank == 0 and not args.no_parity and hasattr(w, "check_gathered"):
+            gather["check"] = w.check_gathered(big, np.random.default_rng(2))
+        del big
+        torch.cuda.empty_cache()
 
     parity = None
     if not args.no_parity and rank == 0:
@@ -657,7 +784,10 @@ def main():
         value = world * w.samples_per_step * args.steps / wall / 1e6
         kern_ms = float(np.mean(ev_ms))
         achieved = w.bytes_per_step / (kern_ms * 1e-3) / 1e9
-        stream = stream_copy_gbps(torch, sd)
+        tol = getattr(w, "tol", 1e-6)
+        parity_ok = parity is None or parity <= tol
+        if gather and gather["check"] is not None:
+            parity_ok = parity_ok and gather["check"] <= tol
         out = {
             "metric": w.metric,
             "value": round(value, 1),
@@ -676,17 +806,27 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic(args.config, args.log2n, w.algo_name, w.kernel),
-                         "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": w.bytes_per_step,
-                         "stream_copy_GBps": round(stream, 1), "frac_of_stream_copy": round(achieved / stream, 4)},
-            "parity": {"check": getattr(w, "parity_check", "rel_rms vs the f64 restatement (tolerance 1e-6, IIR 1e-5)"),
-                       "value": parity},
-            "gather_ms": gather_ms,
+                         "kernel_ms": round(kern_ms, 4), "kernel_ms_median": round(float(np.median(ev_ms)), 4),
+                         "kernel_ms_min": round(float(np.min(ev_ms)), 4),
+                         "algorithmic_bytes_per_launch": w.bytes_per_step,
+                         "stream_copy_GBps": round(copy_gbps, 1), "frac_of_stream_copy": round(achieved / copy_gbps, 4)},
+            "parity": {"check": getattr(w, "parity_check", "rel_rms vs the f64 restatement"),
+                       "value": parity, "tolerance": tol, "ok": parity_ok},
+            "gather": gather,
         }
         if not args.no_cpu:
-            out["cpu_baseline"] = w.cpu(args.cpu_samples or CPU_DEFAULT[args.config])
+            cb = w.cpu(args.cpu_samples or CPU_DEFAULT[args.config])
+            cb["host_nproc"] = os.cpu_count()
+            cb["host_affinity_cpus"] = len(os.sched_getaffinity(0))
+            out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
+        if not parity_ok:
+            print(f"bench.py: parity {parity} (gather check {gather and gather['check']}) exceeds tolerance {tol}",
+                  file=sys.stderr)
     if world > 1:
         dist.destroy_process_group()
+    if rank == 0 and not parity_ok:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

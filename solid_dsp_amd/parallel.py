@@ -51,3 +51,26 @@ def gather_to_root(piece, root: int = 0):
     bufs = [torch.empty_like(piece) for _ in range(dist.get_world_size())] if rank == root else None
     dist.gather(piece.contiguous(), bufs, dst=root)
     return bufs
+
+
+def gather_full_to_root(out, root: int = 0, chunk_bytes: int = 1 << 30):
+    """Gather every rank's whole 1-D output onto `root` as one [world, numel]
+    tensor (None on the other ranks).  The transfer is cut into chunks of at
+    most `chunk_bytes` per rank, each one `gather` straight into the row
+    slices of the result (no staging copy), so RCCL moves large messages
+    point to point over the root's xGMI links.  Every rank passes the same numel."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return out.reshape(1, -1)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    out = out.reshape(-1)
+    if not out.is_contiguous():
+        raise ValueError("gather_full_to_root: output must be contiguous")
+    numel = out.numel()
+    step = max(1, chunk_bytes // out.element_size())
+    big = torch.empty((world, numel), dtype=out.dtype, device=out.device) if rank == root else None
+    for c0 in range(0, numel, step):
+        c1 = min(numel, c0 + step)
+        dist.gather(out[c0:c1], [big[r, c0:c1] for r in range(world)] if rank == root else None, dst=root)
+    return big

@@ -83,3 +83,56 @@ def test_world2_gloo_shard_time_gather():
             x = O.synth(20250226, ch, 0, 4096, complex_=True).astype(np.complex128)
             ref = O.fir(O.RC64, h, 0.2).execute_block(x)
             assert np.array_equal(arr[j], ref)
+
+
+def _full_gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, REPO)
+        from solid_dsp_amd import parallel as P
+        out = torch.arange(1000, dtype=torch.float64) + 1e4 * rank  # ragged last chunk (1000 % 96 != 0)
+        big = P.gather_full_to_root(out, 0, chunk_bytes=96 * 8)
+        if rank == 0:
+            q.put(big.numpy())
+        else:
+            assert big is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_gloo_full_gather_chunks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.spawn(_full_gather_worker, args=(2, _free_port(), q), nprocs=2, join=False)
+    big = q.get(timeout=120)
+    while not pc.join(timeout=60):
+        pass
+    assert big.shape == (2, 1000)
+    for r in range(2):
+        assert np.array_equal(big[r], np.arange(1000) + 1e4 * r)
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """`bench.py --gpus 2` outside torchrun launches two ranks itself (dry run: gloo, CPU)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["ranks"] == [0, 1]
+    assert line["gather_rows"] == 2 and line["gather_ok"]
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-r}
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 run() { local name=$1; local lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${TAG}_$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -${TAILN:-2} gpurun_out/${TAG}_$name.log; ok $rc || exit $rc; }
-if [ -z "$SKIP_TESTS" ]; then run pytest 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; fi
+if [ -z "$SKIP_TESTS" ]; then run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider; fi
 for c in ${CONFIGS:-2 3 4 5}; do
   run bench_cfg$c 300 python bench.py --config $c --steps 10 --warmup 3
   run prof_cfg$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg$c -o run -- python bench.py --config $c --steps 10 --warmup 2 --no-cpu --no-parity
