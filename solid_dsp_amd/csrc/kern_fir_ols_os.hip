@@ -14,24 +14,31 @@
 //  * one segment per 256-thread workgroup, one workgroup per segment (no
 //    persistent loop): the dispatcher deals workgroup b to XCD b % 8, so
 //    segment(b) = lo + (b % 8) q + b / 8 makes every XCD stream one contiguous
-//    eighth of the call in order (a one-shot copy in that order runs at copy
-//    speed, profiles/r01/pattern_probe_7.log; the halo row of a segment is
-//    the tail its XCD neighbour just read, an L2 hit);
-//  * resources for 4 workgroups per CU (16 waves): <= 128 VGPRs and one 34 KB
-//    LDS image + 2 KB twiddle row table.  The image is ALIASED across phases:
-//    in P2/P4 lane (k0, n0) owns the 16 positions (k0, 16 j + n0), in P3 lane
-//    (k0, k1) owns (k0, 16 k1 + j), in P1/P5 lane c owns (k, c) -- each lane
-//    reads and rewrites only its own positions inside a phase, so one region
-//    with the four phase barriers suffices (no second image, no extra barrier);
-//  * no per-lane tables in registers: W4096^(c k) = D_{k>>2} C_{k&3} from six
-//    per-lane bases (C_b = W^(b c), D_a = W^(4 a c)), W256 rows from LDS, the
-//    lane's spectrum slice loaded from L2 during P2 for P3.
+//    eighth of the call in order (the halo row of a segment is the tail its XCD
+//    neighbour just read, an L2 hit).  Measured against the alternatives in
+//    persistent grids (any order) and more or fewer workgroups per
+//    CU are slower;
+//  * 4 workgroups per CU (16 waves): 96 VGPRs and one 34 KB LDS image.  The
+//    image is ALIASED across phases: in P2/P4 lane (k0, n0) owns the 16
+//    positions (k0, 16 j + n0), in P3 lane (k0, k1) owns (k0, 16 k1 + j), in
+//    P1/P5 lane t owns column t -- each lane reads and rewrites only its own
+//    positions inside a phase, so one region suffices.  P2, P3 and P4 of wave w
+//    touch only rows k0 = 4w .. 4w + 3, so only P1 -> P2 and P4 -> P5 need a
+//    workgroup barrier;
+//  * lane t owns column t in P1 / P5: 8-byte buffer loads and stores per row
+//    (row offsets in SGPRs, no address arithmetic in VGPRs);
+//  * no twiddle tables in LDS or per-lane tables in registers: W4096^(t k) =
+//    D_{k>>2} C_{k&3} and W256^(l k) = F_{k>>2} E_{k&3} from per-lane bases
+//    (3 + 3 float4 from L2), the spectrum slice of P3 loaded from L2 in P2.
 //
-// LDS image: element (r, c) (r = row 0..15, c = 0..255, block b = c >> 4,
-// e = c & 15) at r*272 + 16 b + 2 ((e >> 1 ^ b) & 7) + (e & 1).  Rows are 544
-// dwords apart (opposite halves of the 64 banks); the 16-byte pair swizzle by
-// the block index keeps P3's ds_read_b128 / ds_write_b128 and every 8-byte
-// access of P2..P5 conflict-free (P1's ds_write_b64 is 2-way).
+// LDS image: element (r, c) at r * 272 + c + (c >> 4) (one 8-byte pad per
+// 16-column block; rows 544 dwords apart, i.e. opposite halves of the 64
+// banks).  Every access is a per-lane base plus a compile-time offset and is
+// conflict-free except P5's reads (lanes 0 and 31 of a 32-lane group share a
+// bank pair: 3 LDS cycles instead of 2).
+//
+// Numerics: bit-identical across calls and launch shapes; against the f64
+// restatement rel-RMS ~1.8e-7 on the cfg2 taps (§8d tolerance 1e-6).
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 #include "sdsp_pk.hpp"
@@ -44,96 +51,95 @@ namespace {
 
 constexpr int kRow = 272;
 
-__device__ __forceinline__ int opos(int r, int c) {
-    const int b = c >> 4, e = c & 15;
-    return r * kRow + 16 * b + ((((e >> 1) ^ b) & 7) << 1) + (e & 1);
+// WAVE: the next phase reads only what this wave wrote (the LDS operations of one
+// wave complete in order), so a compiler-level fence replaces the block barrier
+template <bool WAVE> __device__ __forceinline__ void phase_sync() {
+    if constexpr (WAVE) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
+typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+constexpr int kBufWord3 = 0x00020000;  // raw buffer descriptor word 3 (gfx9 family)
+
+// x = D_{k>>2} C_{k&3} for C_b = c[b-1], D_a = d[a-1] (k = 0 -> 1)
+__device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k) {
+    const int a = k >> 2, b = k & 3;
+    if (a == 0) return b == 0 ? f2{1.0f, 0.0f} : c[b - 1];
+    if (b == 0) return d[a - 1];
+    return pmul(d[a - 1], c[b - 1]);
 }
 
 }  // namespace
 
-__global__ void __launch_bounds__(256, 4)
-fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
-                  f2* __restrict__ y, long long n, long long lo, long long hi, long long q, int h2) {
-    __shared__ __attribute__((aligned(16))) f2 img[16 * kRow];
-    __shared__ float4 sw2[128];
-    const int t = threadIdx.x;
-    const int xc = blockIdx.x & 7;
-    const long long seg = lo + (long long)xc * q + (blockIdx.x >> 3);
-    const long long xe = lo + (long long)(xc + 1) * q;
-    if (seg >= (xe < hi ? xe : hi)) return;  // uniform over the workgroup
-    const int V = 4096 - 256 * h2;
-    const long long base = (long long)blockIdx.y * n + seg * V - 256 * h2;
-    const int up = (t >> 4) & 1;
-    const int colX = 32 * (t >> 5) + 2 * (t & 15);
-    const int col = colX + up;
+// VAR = 0 is the product kernel; tools/lab.mk builds other values (SDSP_OLS_LAB)
+// for in-process A/B runs -- they are never part of libsdsp.so.  Lab bits:
+// 1 block barriers at the wave-local phase boundaries; 2 no HBM traffic
+// (ablation: outputs dropped); 4 HBM traffic only (ablation: no transform).
+template <int VAR>
+__device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
+                                               const float4* __restrict__ tb, f2* __restrict__ y, long long base,
+                                               int h2, f2* img, int t) {
     const int hi4 = t >> 4, lo4 = t & 15;
-
-    // the segment: lane loads columns colX, colX + 1 of rows 2i + up (16-byte rows)
-    float4 nq[8];
-    {
-        const float4* xb = reinterpret_cast<const float4*>(x + base + 256 * up + colX);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) nq[i] = xb[256 * i];
-    }
-    // twiddle bases of column col, and the W256 row table into LDS (row r, pair p at r*8 + (p ^ r/2))
-    const float4 b0 = tb[col], b1 = tb[256 + col], b2 = tb[512 + col];
-    if (t < 128) {
-        const int r = t >> 3, p = t & 7;
-        sw2[r * 8 + (p ^ (r >> 1))] = tb[768 + t];
-    }
-    f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
-    f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
-    // W4096^(col k) = D_{k>>2} C_{k&3}
-    auto w1 = [&](int k) -> f2 {
-        const int a = k >> 2, b = k & 3;
-        if (a == 0) return b == 0 ? f2{1.0f, 0.0f} : Cb[b - 1];
-        if (b == 0) return Da[a - 1];
-        return pmul(Da[a - 1], Cb[b - 1]);
-    };
-
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, 32768, kBufWord3);
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, 32768, kBufWord3);
+    const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
+    const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0, 2048 * 16, kBufWord3);
     f2 v[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        float4 r = nq[i];
-        swap16(r.x, r.z);
-        swap16(r.y, r.w);
-        v[2 * i] = f2{r.x, r.y};
-        v[2 * i + 1] = f2{r.z, r.w};
+    for (int r = 0; r < 16; ++r) {
+        if constexpr (VAR & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
+        else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
     }
-    // P1: DFT16 n2 -> k0, * W4096^(col k0) -> (k0, col)
+    if constexpr (VAR & 4) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (r >= h2) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[r]), ry, 8 * t, 2048 * r, 0);
+        return;
+    }
+    // twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build)
+    const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 0, 0));
+    const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 4096, 0));
+    const float4 b2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 8192, 0));
+    const float4 e0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12288, 0));
+    const float4 e1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12544, 0));
+    const float4 e2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12800, 0));
+    f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
+    f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
+    const f2 Eb[3] = {f2{e0.x, e0.y}, f2{e0.z, e0.w}, f2{e1.x, e1.y}};
+    const f2 Fa[3] = {f2{e1.z, e1.w}, f2{e2.x, e2.y}, f2{e2.z, e2.w}};
+    f2* col = img + t + (t >> 4);  // (r, t) at col[r * kRow]
+
+    // P1: DFT16 n2 -> k0, * W4096^(t k0) -> (k0, t)
     pdft16<false>(v);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        if (k == 0) img[opos(0, col)] = v[0];
-        else img[opos(k, col)] = pmul(v[kout(k)], w1(k));
-    }
+    for (int k = 0; k < 16; ++k) col[k * kRow] = k == 0 ? v[0] : pmul(v[kout(k)], tw_pair(Cb, Da, k));
     __syncthreads();
 
     // P2: lane (k0 = hi4, n0 = lo4): DFT16 n1 -> k1, * W256^(n0 k1) -> (k0, 16 k1 + n0)
+    f2* r2 = img + hi4 * kRow + lo4;  // (hi4, 16 j + lo4) at r2[17 j]
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = img[opos(hi4, 16 * j + lo4)];
+    for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
     float4 hq[8];  // spectrum slice of lane (k0, k1) = t for P3, k-pair major
 #pragma unroll
-    for (int p = 0; p < 8; ++p) hq[p] = Hs[p * 256 + t];
-    pdft16<false>(v);
-    const float4* w2row = sw2 + lo4 * 8;
+    for (int p = 0; p < 8; ++p) hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+    f2 w2[16];  // W256^(lo4 k), used by P2 (n0 = lo4) and P3 (k1 = lo4)
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        const float4 w = w2row[p ^ (lo4 >> 1)];
-        img[opos(hi4, 16 * (2 * p) + lo4)] = p == 0 ? v[0] : pmul(v[kout(2 * p)], f2{w.x, w.y});
-        img[opos(hi4, 16 * (2 * p + 1) + lo4)] = pmul(v[kout(2 * p + 1)], f2{w.z, w.w});
-    }
-    __syncthreads();
+    for (int k = 1; k < 16; ++k) w2[k] = tw_pair(Eb, Fa, k);
+    pdft16<false>(v);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r2[17 * k] = k == 0 ? v[0] : pmul(v[kout(k)], w2[k]);
+    phase_sync<!(VAR & 1)>();
 
     // P3: lane (k0 = hi4, k1 = lo4) over n0: DFT16 n0 -> k2, * H, IDFT16 k2 -> n0, * conj W256^(k1 n0)
     {
-        float4* row = reinterpret_cast<float4*>(img + hi4 * kRow + 16 * lo4);
+        f2* r3 = img + hi4 * kRow + 17 * lo4;  // (hi4, 16 lo4 + j) at r3[j]
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            const float4 r = row[(p ^ lo4) & 7];
-            v[2 * p] = f2{r.x, r.y};
-            v[2 * p + 1] = f2{r.z, r.w};
-        }
+        for (int j = 0; j < 16; ++j) v[j] = r3[j];
         pdft16<false>(v);
         f2 u[16];
 #pragma unroll
@@ -143,40 +149,55 @@ fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const
         }
         pdft16<true>(u);
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
-            const float4 w = w2row[p ^ (lo4 >> 1)];
-            const f2 a = p == 0 ? u[kout(0)] : pmulc(u[kout(2 * p)], f2{w.x, w.y});
-            const f2 c = pmulc(u[kout(2 * p + 1)], f2{w.z, w.w});
-            row[(p ^ lo4) & 7] = make_float4(a.x, a.y, c.x, c.y);
-        }
+        for (int j = 0; j < 16; ++j) r3[j] = j == 0 ? u[kout(0)] : pmulc(u[kout(j)], w2[j]);
     }
-    __syncthreads();
+    phase_sync<!(VAR & 1)>();
 
     // P4: lane (k0 = hi4, n0 = lo4): IDFT16 k1 -> n1 -> (k0, 16 n1 + n0)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = img[opos(hi4, 16 * j + lo4)];
+    for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
     pdft16<true>(v);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) img[opos(hi4, 16 * k + lo4)] = v[kout(k)];
+    for (int k = 0; k < 16; ++k) r2[17 * k] = v[kout(k)];
     __syncthreads();
 
-    // P5: lane col: * conj W4096^(col k0), IDFT16 k0 -> n2; row n2 at v[kout(n2)].  The bases
-    // are made opaque first so the products are recomputed here rather than kept live from P1.
+    // P5: lane t: * conj W4096^(t k0), IDFT16 k0 -> n2; row n2 at v[kout(n2)].  The bases are
+    // made opaque first so the products are recomputed here rather than kept live from P1.
 #pragma unroll
     for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Cb[i]), "+v"(Da[i]));
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = k == 0 ? img[opos(0, col)] : pmulc(img[opos(k, col)], w1(k));
+    for (int k = 0; k < 16; ++k) v[k] = k == 0 ? col[0] : pmulc(col[k * kRow], tw_pair(Cb, Da, k));
     pdft16<true>(v);
-    float4* yb = reinterpret_cast<float4*>(y + base + 256 * up + colX);
+    if constexpr (VAR & 2) {  // outputs kept live, not stored
+        f2 acc = v[0];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const f2 a = v[kout(2 * i)], c = v[kout(2 * i + 1)];
-        float4 r = make_float4(a.x, a.y, c.x, c.y);
-        swap16(r.x, r.z);
-        swap16(r.y, r.w);
-        if (2 * i + up >= h2) yb[256 * i] = r;  // rows below h2 are the halo
+        for (int r = 1; r < 16; ++r) acc += v[r];
+        if (acc.x == 1.2345e30f) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc), ry, 8 * t, 0, 0);
+        return;
     }
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+        if (r >= h2) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, 0);
 }
+
+template <int VAR>
+__global__ void __launch_bounds__(256, 4)
+fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
+                  f2* __restrict__ y, long long n, long long lo, long long hi, long long q, int h2) {
+    __shared__ __attribute__((aligned(16))) f2 img[16 * kRow];
+    const int xc = blockIdx.x & 7;
+    const long long seg = lo + (long long)xc * q + (blockIdx.x >> 3);
+    const long long xe = lo + (long long)(xc + 1) * q;
+    if (seg >= (xe < hi ? xe : hi)) return;  // uniform over the workgroup
+    const int V = 4096 - 256 * h2;
+    ols_os_segment<VAR>(x, Hs, tb, y, (long long)blockIdx.y * n + seg * V - 256 * h2, h2, img, threadIdx.x);
+}
+
+#ifdef SDSP_OLS_LAB
+static int g_lab_variant = 0;
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int, int) { g_lab_variant = v; }
+#define SDSP_LAB_VARIANTS(X) X(1) X(2) X(3) X(4)
+#endif
 
 hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
                              long long lo, long long hi) {
@@ -184,7 +205,16 @@ hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n,
     if (p.halo_rows < 1 || p.halo_rows > 15) return hipErrorInvalidValue;
     const long long q = (hi - lo + 7) / 8;
     const dim3 grid((unsigned)(8 * q), (unsigned)channels);
-    hipLaunchKernelGGL(fir_ols_os_kernel, grid, dim3(256), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+#ifdef SDSP_OLS_LAB
+#define SDSP_LAB_CASE(V)                                                                                       \
+    if (g_lab_variant == V) {                                                                                  \
+        hipLaunchKernelGGL(fir_ols_os_kernel<V>, grid, dim3(256), 0, s, (const f2*)x, (const float4*)p.d_pkt,  \
+                           (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows);            \
+        return hipGetLastError();                                                                              \
+    }
+    SDSP_LAB_VARIANTS(SDSP_LAB_CASE)
+#endif
+    hipLaunchKernelGGL(fir_ols_os_kernel<0>, grid, dim3(256), 0, s, (const f2*)x, (const float4*)p.d_pkt,
                        (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows);
     return hipGetLastError();
 }

@@ -190,10 +190,10 @@ int ols_build(sdsp_fir* h) {
     SDSP_TRY(h->d_pkt.ensure(pkt.size() * 4), "alloc packed tables");
     SDSP_TRY(hipMemcpyAsync(h->d_pkt.p, pkt.data(), pkt.size() * 4, hipMemcpyHostToDevice, h->stream),
              "copy packed tables");
-    // one-shot kernel: per column c the twiddle bases C_b = W4096^(b c), D_a = W4096^(4 a c)
-    // (b, a = 1..3) as float4 [q][c] = (C1 C2 | C3 D1 | D2 D3), then the W256 rows
-    // float4 [r][p] = (W256^(r 2p), W256^(r (2p + 1)))
-    std::vector<float> os(4 * (768 + 128));
+    // one-shot kernel (kern_fir_ols_os.hip): per column c the twiddle bases C_b = W4096^(b c),
+    // D_a = W4096^(4 a c) (b, a = 1..3) as float4 [q][c] = (C1 C2 | C3 D1 | D2 D3), then per
+    // row l the W256 bases E_b = W256^(b l), F_a = W256^(4 a l) as float4 [768 + 16 q + l]
+    std::vector<float> os(4 * kOlsOsTabF4);
     auto put = [&](size_t f4, int half, long long m, int nn) {
         const double ang = -2.0 * M_PI * (double)(m % nn) / nn;
         os[4 * f4 + 2 * half] = (float)std::cos(ang);
@@ -207,11 +207,14 @@ int ols_build(sdsp_fir* h) {
         put(512 + c, 0, 8LL * c, 4096);
         put(512 + c, 1, 12LL * c, 4096);
     }
-    for (int r = 0; r < 16; ++r)
-        for (int p = 0; p < 8; ++p) {
-            put(768 + r * 8 + p, 0, (long long)r * 2 * p, 256);
-            put(768 + r * 8 + p, 1, (long long)r * (2 * p + 1), 256);
-        }
+    for (int l = 0; l < 16; ++l) {
+        put(768 + l, 0, l, 256);
+        put(768 + l, 1, 2LL * l, 256);
+        put(784 + l, 0, 3LL * l, 256);
+        put(784 + l, 1, 4LL * l, 256);
+        put(800 + l, 0, 8LL * l, 256);
+        put(800 + l, 1, 12LL * l, 256);
+    }
     SDSP_TRY(h->d_ostab.ensure(os.size() * 4), "alloc one-shot tables");
     SDSP_TRY(hipMemcpyAsync(h->d_ostab.p, os.data(), os.size() * 4, hipMemcpyHostToDevice, h->stream),
              "copy one-shot tables");

@@ -32,6 +32,8 @@ constexpr int kOlsOneShot = 0;     // interior segments: one-shot XCD-ordered ke
 constexpr int kOlsPersistent = 1;  // persistent packed kernel, kOlsSegsPerBlock segments per workgroup
 constexpr int kOlsScalar = 2;      // scalar persistent kernel for every segment (kern_fir_ols.hip)
 constexpr int kOlsSegsPerBlock = 16;
+constexpr int kOlsOsTabF4 = 768 + 48;  // W4096 column bases [3][256], W256 row bases [3][16]
+
 struct OlsPlan {
     void* d_H;    // [256][16] c32: H[k0 + 16 k1 + 256 k2] / N * scale, row t = 16 k0 + k1
     void* d_tw1;  // [256][16] c32: W4096^(t*k)
@@ -40,7 +42,7 @@ struct OlsPlan {
     int kernel = kOlsOneShot;
     void* d_pkt = nullptr;    // k-pair major tables: [0, 2048) float4 spectrum rows, [2048, 4096) W4096 rows,
                               // [4096, 4224) W256 rows (runtime.cpp ols_build)
-    void* d_ostab = nullptr;  // one-shot kernel: [3][256] float4 twiddle bases per column
+    void* d_ostab = nullptr;  // one-shot kernel tables (kOlsOsTabF4 float4, runtime.cpp ols_build)
                               // (C1 C2 | C3 D1 | D2 D3), then [16][8] float4 W256 rows
 };
 constexpr int kOlsN = 4096;

@@ -1,0 +1,80 @@
+"""Interleaved in-process A/B of overlap-save one-shot kernel variants (tools
+only): loads tools/_build/libsdsp_lab.so (make -f tools/lab.mk), which carries
+extra template instances of fir_ols_os_kernel selected by
+sdsp_lab_set_ols_variant.  Shuffled order every round, median of rounds
+(guide §5.4 rule 24), after a clock-settling phase.
+
+  OLS_CASES="0,4,4:18432,20::4" OLS_ROUNDS=15 python tools/ols_lab.py
+A case is var[:dyn_lds_bytes[:chunk]].  Variant bits (kern_fir_ols_os.hip): 1
+wave-level sync for the two wave-local phase boundaries; 2 no HBM traffic
+(ablation); 4 HBM traffic only (ablation); 16 XCDs interleaved in runs of
+`chunk` segments instead of contiguous eighths.  dyn_lds pins occupancy
+(36 KB static: +18432 -> 3 workgroups per CU, +45056 -> 2).
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
+    import torch
+    import solid_dsp_amd._lib as LL
+    LL.LIB_PATH = os.path.join(REPO, "tools", "_build", "libsdsp_lab.so")
+    import solid_dsp_amd as sd
+    from solid_dsp_amd import FIRFilter
+    from solid_dsp_amd.filter import firdes
+    L = sd.lib()
+    L.sdsp_lab_set_ols_variant.argtypes = [C.c_int, C.c_int, C.c_int]
+    n = 1 << log2n
+    h = firdes.firdes_kaiser(256, 0.1, 80.0, 0.0).astype(np.float32)
+    d_in = torch.empty(n, dtype=torch.complex64, device="cuda")
+    L.sdsp_synth_f32_device(d_in.data_ptr(), 20250226, 0, 0, 2 * n, None)
+    def parse(c):
+        f = (c.split(":") + ["", ""])[:3]
+        return (int(f[0]), int(f[1] or 0), int(f[2] or 1))
+    variants = [parse(c) for c in os.environ.get("OLS_CASES", "0,1,2,4").split(",")]
+    f = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, algo=sd.ALGO_FFT)
+    s = torch.cuda.current_stream()
+    d_out = torch.empty_like(d_in)
+    outs, diff = {}, {}
+    for v in variants:
+        if v[0] & 6:
+            continue
+        L.sdsp_lab_set_ols_variant(*v)
+        f.reset()
+        f.execute_block_device(d_in, n, d_out, s)
+        outs[v] = np.concatenate([d_out[: 1 << 22].cpu().numpy(), d_out[-(1 << 20):].cpu().numpy()])
+    ref = outs.get((0, 0, 1))
+    for v, o in outs.items():
+        diff[v] = None if ref is None else float(np.linalg.norm(o.astype(np.complex128) - ref) / np.linalg.norm(ref))
+    L.sdsp_lab_set_ols_variant(0, 0, 1)
+    for _ in range(60):  # ~0.2 s of device time: clocks settle
+        f.execute_block_device(d_in, n, d_out, s)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(1)
+    times = {v: [] for v in variants}
+    order = list(variants)
+    for _ in range(rounds):
+        rng.shuffle(order)
+        for v in order:
+            L.sdsp_lab_set_ols_variant(*v)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            f.execute_block_device(d_in, n, d_out, s)
+            e1.record(s)
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1))
+    res = {"var%d:%d:%d" % v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                       "frac_of_8TBps": 16.0 * n / (np.median(t) * 1e-3) / 8e12,
+                       "rel_diff_vs_var0": diff.get(v)} for v, t in times.items()}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
