@@ -17,6 +17,7 @@ SURVEY §8f rows (build-defined cases, same parity + measurement fields):
   7  NCO mix_down, c32, 2^30 samples
   8  batched 2^20-point forward FFT (four-step), c32, 2^28 samples
   9  AGC bank, Complex<f64>, 2^18 channels x 2^10 samples
+ 10  32x interpolating FIR (K = 8), crcf, 2^25 inputs -> 2^30 outputs
 
 With N ranks each rank processes its own independent channel(s) (weak
 scaling, no collective in the timed region); RCCL is used afterwards only for
@@ -49,7 +50,7 @@ def parse():
                    help="ranks (one per GPU); outside torch.distributed.run this process spawns them itself")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5, 6, 7, 8, 9])
+    p.add_argument("--config", type=int, default=2, choices=list(range(1, 11)))
     p.add_argument("--log2n", type=int, default=30, help="samples per GPU per step (configs 2-4)")
     p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"], help="config 2 kernel")
     p.add_argument("--cpu-samples", type=int, default=None,
@@ -638,9 +639,83 @@ class Cfg9AGC:
                          "libm exp/ln/log10)", samples, CPU_CHUNK // 4)
 
 
-WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT, 9: Cfg9AGC}
+class Cfg10Interp:
+    """M=32 interpolator, firdes_kaiser(256, 1/64, 80) rounded to f32 (K = 8 taps per branch),
+    crcf, 2^25 inputs -> 2^30 outputs per GPU (src/filter/fir/interp.rs:102-111)."""
+    metric = "Msamples/sec (outputs) 32x interpolating FIR, 8 taps/branch, crcf; % HBM roofline"
+    tol = 1e-6
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import InterpolatingFIRFilter
+        from solid_dsp_amd.filter import firdes
+        self.M = 32
+        self.n = 1 << (args.log2n - 5)
+        self.h = firdes.firdes_kaiser(256, 1.0 / 64, 80.0, 0.0).astype(np.float32)
+        self.make = lambda d=dev: InterpolatingFIRFilter(self.h, self.M, sample_dtype=np.complex64, device=d)
+        self.f = self.make()
+        self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
+        self.d_out = torch.empty(self.n * self.M, dtype=torch.complex64, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n * self.M
+        self.bytes_per_step = 8 * self.n + 8 * self.n * self.M
+        self.dtype = "c32 (f32 taps x complex-f32 samples, reference summation order)"
+        self.kernel = "interp_tile_kernel<float, c32, EXACT, 8> (LDS-staged inputs, branch pairs in registers, 16-byte stores)"
+        self.parity_check = "rel_rms of 4 random 4096-output windows vs the f64 restatement (tolerance 1e-6)"
+        self.workload = f"cfg10: InterpolatingFIRFilter M=32, 256 taps (K=8), crcf, 2^{args.log2n - 5} inputs per channel"
+        self.algo_name = "interp"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def _ref(self, x, j0, count):
+        """outputs for inputs j0 .. j0+count-1 from x[j0-7 .. j0+count) in f64 (zero before 0)"""
+        import oracle_lib as O
+        g = O.interp(O.RC64, self.h.astype(np.float64), self.M)
+        return g.execute_block(x.astype(np.complex128))[7 * self.M:]
+
+    def parity(self, stream, rng, windows=4, width=128):
+        import torch
+        g = self.make()
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        worst = 0.0
+        for _ in range(windows):
+            j = int(rng.integers(8, self.n - width))
+            xs = self.d_in[j - 7: j + width].cpu().numpy()
+            ref = self._ref(xs, j, width)
+            ys = self.d_out[j * self.M: (j + width) * self.M].cpu().numpy()
+            worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
+        return worst
+
+    def check_gathered(self, big, rng, width=128):
+        import oracle_lib as O
+        worst = 0.0
+        for r in range(big.shape[0]):
+            j = int(rng.integers(8, self.n - width))
+            xs = O.synth(SEED, r, j - 7, width + 7, complex_=True)
+            ys = big[r, j * self.M: (j + width) * self.M].cpu().numpy()
+            ref = self._ref(xs, j, width)
+            worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
+        return worst
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        chunk = CPU_CHUNK // self.M
+        x = O.synth(SEED, 0, 0, chunk, complex_=True).astype(np.complex128)
+        f = O.interp(O.RC64, self.h.astype(np.float64), self.M)
+        r = timed_cpu(lambda c: f.execute_block(x), "InterpolatingFIRFilter<f64, Complex<f64>> restatement (push + "
+                      "M DotProducts over Window::to_vec per input)", samples // self.M, chunk)
+        r["value"] *= self.M  # outputs per second, the metric's unit
+        r["sample"] += f"; value counts the {self.M} outputs per input"
+        return r
+
+
+WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT, 9: Cfg9AGC,
+             10: Cfg10Interp}
 # bounded CPU samples: about 10-20 s of single-thread work each on a current x86 host
-CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 << 25, 7: 1 << 28, 8: 1 << 24, 9: 1 << 25}
+CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 << 25, 7: 1 << 28, 8: 1 << 24, 9: 1 << 25,
+               10: 1 << 30}
 CPU_CHUNK = 1 << 22
 
 

@@ -204,8 +204,15 @@ SDSP_API int sdsp_pfb_push(sdsp_pfb* h, const void* sample);
 SDSP_API int sdsp_pfb_execute(sdsp_pfb* h, size_t index, void* out);
 /* reset  pfb.rs:77-79 */
 SDSP_API int sdsp_pfb_reset(sdsp_pfb* h);
+/* dot-product order: SDSP_ALGO_EXACT (default, the reference's sequential sum,
+ * bit-identical) or SDSP_ALGO_FMA (fused multiply-add, same order) */
+SDSP_API int sdsp_pfb_set_algo(sdsp_pfb* h, int algo);
+/* independent channels in one handle: blocks are channel-major [channels][n]
+ * in, [channels][n*M] out; resets every channel's window */
+SDSP_API int sdsp_pfb_set_channels(sdsp_pfb* h, size_t channels);
 /* for each input: push, then all M branch outputs -> out[n*M]
- * (InterpolatingFIRFilter::execute_block  interp.rs:102-111) */
+ * (InterpolatingFIRFilter::execute_block  interp.rs:102-111).  The _device form
+ * rejects overlapping input and output blocks (SDSP_E_INVALID_ARGUMENT). */
 SDSP_API int sdsp_pfb_execute_block(sdsp_pfb* h, const void* in, size_t n, void* out);
 SDSP_API int sdsp_pfb_execute_block_device(sdsp_pfb* h, const void* d_in, size_t n, void* d_out, void* stream);
 SDSP_API int sdsp_pfb_frequency_response(const sdsp_pfb* h, double f, double* re_im);

@@ -43,8 +43,99 @@ pfb_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* __restr
     }
 }
 
+// Tiled form for M = 2^m (8 <= M <= 512) and K in {4, 8, 16}: the interpolator
+// shape (InterpolatingFIRFilter::execute_block, one input in, M outputs out).
+// A 256-lane workgroup owns T = 16 * 512 / M consecutive inputs of one channel
+// (XCD-ordered: each XCD streams one contiguous stretch of the output).  Lane
+// (g, q) -- q = 0 .. M/2-1 a pair of branches (2q, 2q + 1), g = 0 .. 512/M - 1
+// a run of R = 16 inputs -- keeps its 2K branch coefficients and the R + K - 1
+// samples its run needs in registers (staged once through LDS, read as
+// wave-broadcasts) and writes its 2R outputs as 16-byte stores: for one input
+// the M/2 lanes of a run cover M contiguous outputs.  Every output is the
+// reference dot product sum_{i<K} cb[p][i] x[j-i] in the reference order.
+constexpr int kInterpR = 16;
+
+template <typename I> struct alignas(2 * sizeof(I)) Pair {
+    I a, b;
+};
+
+template <typename C, typename I, bool EXACT, int K>
+__global__ void __launch_bounds__(256)
+interp_tile_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* __restrict__ cb,
+                   I* __restrict__ y, long long n, int M, int H, long long q8) {
+    constexpr int R = kInterpR;
+    __shared__ I xs[1024 + 16];  // T + K - 1 <= 16 * 64 + 15 samples (M >= 8)
+    const int ch = blockIdx.y;
+    const int xc = blockIdx.x & 7;
+    const long long tile = (long long)xc * q8 + (blockIdx.x >> 3);
+    const int P = M >> 1, G = 256 / P, T = G * R;
+    const long long j0 = tile * T;
+    if (j0 >= n) return;  // uniform
+    x += (long long)ch * n;
+    hist += (long long)ch * H;
+    y += (long long)ch * n * M;
+    const int t = threadIdx.x;
+    // stage x[j0 - K + 1, j0 + T) (zero past n, history before 0)
+    for (int i = t; i < T + K - 1; i += 256) {
+        const long long j = j0 - (K - 1) + i;
+        xs[i] = j < n ? pfb_ext(x, hist, j, H) : zero_v<I>();
+    }
+    const int g = t / P, q = t - g * P;
+    C c0[K], c1[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        c0[i] = cb[(long long)(2 * q) * K + i];
+        c1[i] = cb[(long long)(2 * q + 1) * K + i];
+    }
+    __syncthreads();
+    I w[R + K - 1];  // w[m] = x[jg - K + 1 + m], jg = j0 + g R
+#pragma unroll
+    for (int m = 0; m < R + K - 1; ++m) w[m] = xs[g * R + m];
+    const long long jg = j0 + (long long)g * R;
+    I* yo = y + jg * M + 2 * q;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        I a0 = zero_v<I>(), a1 = zero_v<I>();
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const I s = w[r + K - 1 - i];  // x[jg + r - i]
+            a0 = mac<EXACT>(a0, c0[i], s);
+            a1 = mac<EXACT>(a1, c1[i], s);
+        }
+        if (jg + r < n) *reinterpret_cast<Pair<I>*>(yo + (long long)r * M) = Pair<I>{a0, a1};
+    }
+}
+
+template <typename C, typename I, bool EXACT>
+hipError_t launch_interp_tile(const PfbArgs& a, hipStream_t s) {
+    const int P = a.M / 2, T = (256 / P) * kInterpR;
+    const long long tiles = ((long long)a.n + T - 1) / T;
+    const long long q8 = (tiles + 7) / 8;
+    if (8 * q8 > 0x7fffffffLL) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)(8 * q8), (unsigned)a.channels);
+#define SDSP_INTERP_K(KK)                                                                                        \
+    if (a.K == KK) {                                                                                             \
+        hipLaunchKernelGGL((interp_tile_kernel<C, I, EXACT, KK>), grid, dim3(256), 0, s, (const I*)a.x,          \
+                           (const I*)a.hist, (const C*)a.cb, (I*)a.y, (long long)a.n, a.M, a.H, q8);             \
+        return hipGetLastError();                                                                                \
+    }
+    SDSP_INTERP_K(4)
+    SDSP_INTERP_K(8)
+    SDSP_INTERP_K(16)
+#undef SDSP_INTERP_K
+    return hipErrorInvalidValue;
+}
+
+template <typename I>
+bool interp_tile_applies(const PfbArgs& a) {
+    return a.M >= 8 && a.M <= 512 && (a.M & (a.M - 1)) == 0 && (a.K == 4 || a.K == 8 || a.K == 16) &&
+           a.H == a.K && ((uintptr_t)a.y % (2 * sizeof(I))) == 0;
+}
+
 template <typename C, typename I>
 hipError_t launch_pfb_t(const PfbArgs& a, hipStream_t s) {
+    if (interp_tile_applies<I>(a))
+        return a.exact ? launch_interp_tile<C, I, true>(a, s) : launch_interp_tile<C, I, false>(a, s);
     const long long total = (long long)a.n * a.M;
     long long blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;

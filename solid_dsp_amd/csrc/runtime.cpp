@@ -595,12 +595,14 @@ struct sdsp_pfb {
     int cur = 0;
     int algo = SDSP_ALGO_EXACT;
     hipStream_t stream = nullptr;
+    mutable StreamFence fence;  // last caller stream an execute call was queued on
     DevBuf stage_in, stage_out;
 };
 
 namespace {
 
 int pfb_alloc_state(sdsp_pfb* h) {
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const size_t hb = h->channels * h->K * sample_bytes(h->dtype);
     for (int i = 0; i < 2; ++i) {
         SDSP_TRY(h->d_hist[i].ensure(hb), "alloc window");
@@ -731,7 +733,8 @@ int sdsp_pfb_clone(const sdsp_pfb* h, sdsp_pfb** out) {
     st = pfb_alloc_state(c);
     if (st) { sdsp_pfb_destroy(c); return st; }
     const size_t hb = h->channels * h->K * sample_bytes(h->dtype);
-    e = hipStreamSynchronize(h->stream);
+    e = h->fence.wait();
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e == hipSuccess) e = hipMemcpy(c->d_hist[0].p, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToDevice);
     if (e != hipSuccess) { st = device_status(e, "pfb clone state"); sdsp_pfb_destroy(c); return st; }
     *out = c;
@@ -756,11 +759,29 @@ int sdsp_pfb_coefficients(const sdsp_pfb* h, void* out) {
     return SDSP_OK;
 }
 
+int sdsp_pfb_set_algo(sdsp_pfb* h, int algo) {
+    if (!h || (algo != SDSP_ALGO_EXACT && algo != SDSP_ALGO_FMA)) return SDSP_E_INVALID_ARGUMENT;
+    h->algo = algo;
+    return SDSP_OK;
+}
+
+int sdsp_pfb_set_channels(sdsp_pfb* h, size_t channels) {
+    if (!h || channels == 0) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    h->channels = channels;
+    return pfb_alloc_state(h);
+}
+
 int sdsp_pfb_execute_block_device(sdsp_pfb* h, const void* d_in, size_t n, void* d_out, void* stream) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (n == 0) return SDSP_OK;
     DeviceGuard g(h->device);
     hipStream_t s = pick(stream, h->stream);
+    const size_t sb = sample_bytes(h->dtype);
+    if (ranges_overlap(d_in, h->channels * n * sb, d_out, h->channels * n * h->M * sb)) {
+        set_error("input and output blocks overlap (in-place filtering is not supported)");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
     PfbArgs a{d_in, h->d_hist[h->cur].p, h->d_cb.p, d_out, n, h->channels, (int)h->K, (int)h->M, (int)h->K,
               h->algo != SDSP_ALGO_FMA};
     SDSP_TRY(launch_pfb(h->dtype, a, s), "pfb");
@@ -768,6 +789,7 @@ int sdsp_pfb_execute_block_device(sdsp_pfb* h, const void* d_in, size_t n, void*
                                 h->channels, s),
              "window update");
     h->cur ^= 1;
+    if (s != h->stream) SDSP_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 
@@ -775,6 +797,7 @@ int sdsp_pfb_execute_block(sdsp_pfb* h, const void* in, size_t n, void* out) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (n == 0) return SDSP_OK;
     DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const size_t sb = sample_bytes(h->dtype);
     SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
     SDSP_TRY(h->stage_out.ensure(h->channels * n * h->M * sb), "stage out");
@@ -790,6 +813,7 @@ int sdsp_pfb_execute_block(sdsp_pfb* h, const void* in, size_t n, void* out) {
 int sdsp_pfb_push(sdsp_pfb* h, const void* sample) {
     if (!h || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const size_t sb = sample_bytes(h->dtype);
     SDSP_TRY(h->stage_in.ensure(sb), "stage in");
     SDSP_TRY(hipMemcpyAsync(h->stage_in.p, sample, sb, hipMemcpyHostToDevice, h->stream), "H2D");
@@ -804,6 +828,7 @@ int sdsp_pfb_push(sdsp_pfb* h, const void* sample) {
 int sdsp_pfb_execute(sdsp_pfb* h, size_t index, void* out) {
     if (!h || h->channels != 1 || index >= h->M) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     const size_t sb = sample_bytes(h->dtype);
     SDSP_TRY(h->stage_out.ensure(h->M * sb), "stage out");
     // all branches on the current window: x = newest sample, history = the K-1 before it

@@ -218,7 +218,8 @@ class DecimatingFIRFilter(_FirBase):
 class PolyPhaseFilterBank:
     """PolyPhaseFilterBank<Coef, In>  (src/filter/fir/pfb.rs:3-91)."""
 
-    def __init__(self, coefs, filters, scale=1.0, sample_dtype=None, coef_dtype=None, device=0, _interp=None):
+    def __init__(self, coefs, filters, scale=1.0, sample_dtype=None, coef_dtype=None, device=0, _interp=None,
+                 algo=None, channels=1):
         c = _coef_array(coefs, coef_dtype)
         if sample_dtype is None:
             sample_dtype = _default_sample(c.dtype)
@@ -233,6 +234,11 @@ class PolyPhaseFilterBank:
             L.check(L.lib().sdsp_interp_create(C.byref(h), self.dtype, L.ptr(c), len(c), _interp, device))
         self._h = h
         self.device = device
+        self.channels = channels
+        if algo is not None:
+            L.check(L.lib().sdsp_pfb_set_algo(self._h, algo))
+        if channels != 1:
+            L.check(L.lib().sdsp_pfb_set_channels(self._h, channels))
 
     @classmethod
     def new(cls, coefs, filters, scale, **kw):
@@ -293,16 +299,21 @@ class PolyPhaseFilterBank:
         return out[0]
 
     def execute_block(self, samples) -> np.ndarray:
-        """push each sample then emit all M branch outputs (out[n*M + p])."""
+        """push each sample then emit all M branch outputs (out[n*M + p]); channel-major
+        [channels, n] -> [channels, n*M] when channels > 1."""
         x = np.ascontiguousarray(samples, dtype=self.sample_dtype)
-        y = np.zeros(len(x) * self.len(), dtype=self.sample_dtype)
-        if len(x):
-            L.check(L.lib().sdsp_pfb_execute_block(self._h, L.ptr(x), len(x), L.ptr(y)))
+        if self.channels > 1 and (x.ndim != 2 or x.shape[0] != self.channels):
+            raise ValueError("multi-channel input must be [channels, n]")
+        n = x.shape[-1]
+        y = np.zeros((self.channels, n * self.len()) if self.channels > 1 else n * self.len(), dtype=self.sample_dtype)
+        if n:
+            L.check(L.lib().sdsp_pfb_execute_block(self._h, L.ptr(x), n, L.ptr(y)))
         return y
 
     def execute_block_device(self, d_in, n: int, d_out, stream=None):
-        pin = L.device_ptr(d_in, self.sample_dtype, n, self.device, "input")
-        pout = L.device_ptr(d_out, self.sample_dtype, n * self.len(), self.device, "output")
+        """n inputs per channel ([channels][n] in, [channels][n*M] out), device resident."""
+        pin = L.device_ptr(d_in, self.sample_dtype, self.channels * n, self.device, "input")
+        pout = L.device_ptr(d_out, self.sample_dtype, self.channels * n * self.len(), self.device, "output")
         L.check(L.lib().sdsp_pfb_execute_block_device(self._h, pin, n, pout, L.stream_handle(stream)))
         return n * self.len()
 
@@ -313,8 +324,9 @@ class PolyPhaseFilterBank:
 class InterpolatingFIRFilter(PolyPhaseFilterBank):
     """InterpolatingFIRFilter<Coef, In>  (src/filter/fir/interp.rs:6-138)."""
 
-    def __init__(self, coefs, interpolation, sample_dtype=None, coef_dtype=None, device=0):
-        super().__init__(coefs, interpolation, 1.0, sample_dtype, coef_dtype, device, _interp=interpolation)
+    def __init__(self, coefs, interpolation, sample_dtype=None, coef_dtype=None, device=0, algo=None, channels=1):
+        super().__init__(coefs, interpolation, 1.0, sample_dtype, coef_dtype, device, _interp=interpolation,
+                         algo=algo, channels=channels)
         self._interpolation = interpolation
 
     @classmethod

@@ -408,3 +408,46 @@ def test_device_synth_matches_host():
     got = to_host(d)
     ref = O.synth(20250226, 5, 1000, n)
     assert bits_equal(got, ref)
+
+
+# ---------------------------------------------------------------- tiled interpolator (M = 2^m >= 8, K in {4, 8, 16})
+@pytest.mark.parametrize("dt,cdt,sdt", DTYPES)
+@pytest.mark.parametrize("L,M", [(32, 8), (256, 32), (60, 16), (256, 16), (4096, 512), (512, 64)])
+def test_interp_tiled_exact_bit_parity(dt, cdt, sdt, L, M):
+    """ragged calls across tile boundaries (T = 16 * 512 / M inputs per workgroup), K = ceil_f32(L / M)"""
+    rng = np.random.default_rng(L + M + dt)
+    h = rand(rng, L, cdt)
+    x = rand(rng, 3001, sdt)
+    f = InterpolatingFIRFilter(h, M, sample_dtype=sdt)
+    assert f.subfilter_len() in (4, 8, 16)
+    o = O.interp(dt, h, M)
+    for a, b in [(0, 1), (1, 2), (2, 1030), (1030, 1031), (1031, 3001)]:
+        assert bits_equal(f.execute_block(x[a:b]), o.execute_block(x[a:b])), (a, b)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", [(O.RC32, F32, C64), (O.CC32, C64, C64), (O.RC64, F64, C128)])
+def test_interp_tiled_fma_and_channels(dt, cdt, sdt):
+    import torch
+    rng = np.random.default_rng(dt)
+    M, L, ch, n = 32, 256, 3, 5000
+    h = rand(rng, L, cdt)
+    x = rand(rng, ch * n, sdt).reshape(ch, n)
+    f = InterpolatingFIRFilter(h, M, sample_dtype=sdt, algo=sd.ALGO_FMA, channels=ch)
+    d_in = to_dev(x.reshape(-1))
+    d_out = empty_dev(ch * n * M, sdt)
+    f.execute_block_device(d_in[: ch * n], n, d_out)
+    torch.cuda.synchronize()
+    y = to_host(d_out).reshape(ch, n * M)
+    tol = 1e-6 if np.dtype(sdt) == np.complex64 else 1e-13
+    for c in range(ch):
+        ref = O.interp(O.CC64 if np.dtype(cdt).kind == "c" else O.RC64, h.astype(C128 if np.dtype(cdt).kind == "c" else F64),
+                       M).execute_block(x[c].astype(C128))
+        assert rel_rms(y[c], ref) <= tol
+
+
+def test_pfb_rejects_in_place():
+    import torch
+    f = InterpolatingFIRFilter(np.ones(64, F32), 8, sample_dtype=C64)
+    buf = torch.zeros(8 * 100, dtype=torch.complex64, device="cuda")
+    with pytest.raises(sd.SdspError):
+        f.execute_block_device(buf, 100, buf)
