@@ -1,0 +1,118 @@
+//! Raw declarations of include/sdsp.h (C ABI of libsdsp.so).  Every handle is
+//! opaque; samples are `#[repr(C)]` `num::Complex<T>` = interleaved {re, im}.
+#![allow(non_camel_case_types)]
+use std::os::raw::{c_char, c_int, c_void};
+
+#[repr(C)] pub struct sdsp_fir { _p: [u8; 0] }
+#[repr(C)] pub struct sdsp_pfb { _p: [u8; 0] }
+#[repr(C)] pub struct sdsp_iir { _p: [u8; 0] }
+#[repr(C)] pub struct sdsp_fft { _p: [u8; 0] }
+#[repr(C)] pub struct sdsp_chan { _p: [u8; 0] }
+
+pub const SDSP_RR32: c_int = 0;
+pub const SDSP_RC32: c_int = 1;
+pub const SDSP_CC32: c_int = 2;
+pub const SDSP_RR64: c_int = 3;
+pub const SDSP_RC64: c_int = 4;
+pub const SDSP_CC64: c_int = 5;
+
+pub const SDSP_ALGO_AUTO: c_int = 0;
+pub const SDSP_ALGO_EXACT: c_int = 1;
+pub const SDSP_ALGO_FMA: c_int = 2;
+pub const SDSP_ALGO_FFT: c_int = 3;
+
+pub const SDSP_OK: c_int = 0;
+pub const SDSP_E_COEFFICIENTS_LENGTH_ZERO: c_int = 1;
+pub const SDSP_E_DECIMATION_LESS_THAN_ONE: c_int = 2;
+pub const SDSP_E_INTERPOLATION_LESS_THAN_ONE: c_int = 3;
+pub const SDSP_E_NOT_ENOUGH_FILTERS: c_int = 4;
+pub const SDSP_E_NUMERATOR_LENGTH_ZERO: c_int = 10;
+pub const SDSP_E_DENOMINATOR_LENGTH_ZERO: c_int = 11;
+pub const SDSP_E_SOS_SIZE_ZERO: c_int = 12;
+pub const SDSP_E_SOS_SIZE_MISMATCH: c_int = 13;
+pub const SDSP_E_SOS_SIZE_NOT_MULTIPLE_OF_3: c_int = 14;
+pub const SDSP_E_IIR_DECIMATION_LESS_THAN_ONE: c_int = 15;
+pub const SDSP_E_IIR_INTERPOLATION_LESS_THAN_ONE: c_int = 16;
+
+extern "C" {
+    pub fn sdsp_last_error() -> *const c_char;
+    pub fn sdsp_device_count() -> c_int;
+
+    // FIRFilter / DecimatingFIRFilter (fir/mod.rs:58-304, fir/decim.rs:5-281)
+    pub fn sdsp_fir_create(out: *mut *mut sdsp_fir, dtype: c_int, taps: *const c_void, len: usize,
+                           scale: *const c_void, device: c_int) -> c_int;
+    pub fn sdsp_decim_create(out: *mut *mut sdsp_fir, dtype: c_int, taps: *const c_void, len: usize,
+                             scale: *const c_void, decimation: usize, device: c_int) -> c_int;
+    pub fn sdsp_fir_destroy(h: *mut sdsp_fir);
+    pub fn sdsp_fir_clone(h: *const sdsp_fir, out: *mut *mut sdsp_fir) -> c_int;
+    pub fn sdsp_fir_set_algo(h: *mut sdsp_fir, algo: c_int) -> c_int;
+    pub fn sdsp_fir_set_scale(h: *mut sdsp_fir, scale: *const c_void) -> c_int;
+    pub fn sdsp_fir_get_scale(h: *const sdsp_fir, scale: *mut c_void) -> c_int;
+    pub fn sdsp_fir_len(h: *const sdsp_fir) -> usize;
+    pub fn sdsp_fir_decimation(h: *const sdsp_fir) -> usize;
+    pub fn sdsp_fir_coefficients(h: *const sdsp_fir, out: *mut c_void) -> c_int;
+    pub fn sdsp_fir_output_count(h: *const sdsp_fir, n: usize) -> usize;
+    pub fn sdsp_fir_execute_block(h: *mut sdsp_fir, input: *const c_void, n: usize, out: *mut c_void,
+                                  n_out: *mut usize) -> c_int;
+    pub fn sdsp_fir_execute_block_device(h: *mut sdsp_fir, d_in: *const c_void, n: usize, d_out: *mut c_void,
+                                         n_out: *mut usize, stream: *mut c_void) -> c_int;
+    pub fn sdsp_decim_push(h: *mut sdsp_fir, sample: *const c_void) -> c_int;
+    pub fn sdsp_decim_write(h: *mut sdsp_fir, samples: *const c_void, n: usize) -> c_int;
+    pub fn sdsp_fir_reset(h: *mut sdsp_fir) -> c_int;
+    pub fn sdsp_fir_frequency_response(h: *const sdsp_fir, f: f64, re_im: *mut f64) -> c_int;
+    pub fn sdsp_fir_group_delay(h: *const sdsp_fir, f: f64, delay: *mut f64) -> c_int;
+
+    // PolyPhaseFilterBank / InterpolatingFIRFilter (fir/pfb.rs:3-91, fir/interp.rs:6-138)
+    pub fn sdsp_pfb_create(out: *mut *mut sdsp_pfb, dtype: c_int, taps: *const c_void, len: usize,
+                           filters: usize, scale: *const c_void, device: c_int) -> c_int;
+    pub fn sdsp_interp_create(out: *mut *mut sdsp_pfb, dtype: c_int, taps: *const c_void, len: usize,
+                              interpolation: usize, device: c_int) -> c_int;
+    pub fn sdsp_pfb_destroy(h: *mut sdsp_pfb);
+    pub fn sdsp_pfb_clone(h: *const sdsp_pfb, out: *mut *mut sdsp_pfb) -> c_int;
+    pub fn sdsp_pfb_len(h: *const sdsp_pfb) -> usize;
+    pub fn sdsp_pfb_subfilter_len(h: *const sdsp_pfb) -> usize;
+    pub fn sdsp_pfb_set_scale(h: *mut sdsp_pfb, scale: *const c_void) -> c_int;
+    pub fn sdsp_pfb_get_scale(h: *const sdsp_pfb, scale: *mut c_void) -> c_int;
+    pub fn sdsp_pfb_coefficients(h: *const sdsp_pfb, out_mk: *mut c_void) -> c_int;
+    pub fn sdsp_pfb_push(h: *mut sdsp_pfb, sample: *const c_void) -> c_int;
+    pub fn sdsp_pfb_execute(h: *mut sdsp_pfb, index: usize, out: *mut c_void) -> c_int;
+    pub fn sdsp_pfb_reset(h: *mut sdsp_pfb) -> c_int;
+    pub fn sdsp_pfb_execute_block(h: *mut sdsp_pfb, input: *const c_void, n: usize, out: *mut c_void) -> c_int;
+    pub fn sdsp_pfb_frequency_response(h: *const sdsp_pfb, f: f64, re_im: *mut f64) -> c_int;
+    pub fn sdsp_pfb_group_delay(h: *const sdsp_pfb, f: f64, delay: *mut f64) -> c_int;
+
+    // IIRFilter / DecimatingIIRFilter / InterpolatingIIRFilter (iir/mod.rs:62-414, iir/decim.rs, iir/interp.rs)
+    pub fn sdsp_iir_create(out: *mut *mut sdsp_iir, dtype: c_int, ff: *const c_void, nff: usize,
+                           fb: *const c_void, nfb: usize, kind: c_int, device: c_int) -> c_int;
+    pub fn sdsp_iir_decim_create(out: *mut *mut sdsp_iir, dtype: c_int, ff: *const c_void, nff: usize,
+                                 fb: *const c_void, nfb: usize, kind: c_int, decimation: usize,
+                                 device: c_int) -> c_int;
+    pub fn sdsp_iir_interp_create(out: *mut *mut sdsp_iir, dtype: c_int, ff: *const c_void, nff: usize,
+                                  fb: *const c_void, nfb: usize, kind: c_int, interpolation: usize,
+                                  device: c_int) -> c_int;
+    pub fn sdsp_iir_destroy(h: *mut sdsp_iir);
+    pub fn sdsp_iir_clone(h: *const sdsp_iir, out: *mut *mut sdsp_iir) -> c_int;
+    pub fn sdsp_iir_set_algo(h: *mut sdsp_iir, algo: c_int) -> c_int;
+    pub fn sdsp_iir_output_count(h: *const sdsp_iir, n: usize) -> usize;
+    pub fn sdsp_iir_execute_block(h: *mut sdsp_iir, input: *const c_void, n: usize, out: *mut c_void,
+                                  n_out: *mut usize) -> c_int;
+    pub fn sdsp_iir_reset(h: *mut sdsp_iir) -> c_int;
+    pub fn sdsp_iir_frequency_response(h: *const sdsp_iir, f: f64, re_im: *mut f64) -> c_int;
+    pub fn sdsp_iir_group_delay(h: *const sdsp_iir, f: f64, delay: *mut f64) -> c_int;
+
+    // FFT (fft/mod.rs:123-215), channeliser
+    pub fn sdsp_fft_create(out: *mut *mut sdsp_fft, nfft: usize, direction: c_int, precision: c_int,
+                           device: c_int) -> c_int;
+    pub fn sdsp_fft_destroy(h: *mut sdsp_fft);
+    pub fn sdsp_fft_len(h: *const sdsp_fft) -> usize;
+    pub fn sdsp_fft_execute(h: *mut sdsp_fft, input: *const c_void, out: *mut c_void, batch: usize) -> c_int;
+    pub fn sdsp_chan_create(out: *mut *mut sdsp_chan, dtype: c_int, taps: *const c_void, len: usize,
+                            channels: usize, device: c_int) -> c_int;
+    pub fn sdsp_chan_destroy(h: *mut sdsp_chan);
+    pub fn sdsp_chan_execute_block(h: *mut sdsp_chan, input: *const c_void, n: usize, out: *mut c_void,
+                                   frames: *mut usize) -> c_int;
+
+    // DotProduct (dot_product/mod.rs:37-171)
+    pub fn sdsp_dot_execute(dtype: c_int, coefs: *const c_void, len: usize, direction: c_int,
+                            samples: *const c_void, n: usize, out: *mut c_void) -> c_int;
+}

@@ -69,3 +69,15 @@ def test_cfg5_prototype_design_is_finite():
     from solid_dsp_amd.filter import firdes
     h = firdes.firdes_kaiser(8192, 1 / 2048, 80.0, 0.0)
     assert np.all(np.isfinite(h)) and abs(h.sum() - 1024) < 5
+
+
+def test_rust_shim_binds_only_declared_symbols():
+    """rust/solid-sdsp/src/sys.rs (the uncompiled Rust side of the boundary) declares
+    only entry points that include/sdsp.h exports."""
+    import re
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(repo, "include", "sdsp.h")).read()
+    declared = set(re.findall(r"SDSP_API[^;(]*?\b(sdsp_\w+)\s*\(", hdr))
+    rs = open(os.path.join(repo, "rust", "solid-sdsp", "src", "sys.rs")).read()
+    bound = set(re.findall(r"pub fn (sdsp_\w+)\s*\(", rs))
+    assert bound and not (bound - declared), sorted(bound - declared)
