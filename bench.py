@@ -58,6 +58,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--no-gather", action="store_true", help="skip the final RCCL gather of every rank's output")
+    p.add_argument("--no-dropin", action="store_true", help="config 2: skip the drop-in cost figures")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU-only rehearsal of the rank launch, timing and gather over gloo (no GPU)")
     return p.parse_args()
@@ -711,6 +712,63 @@ class Cfg10Interp:
         return r
 
 
+def dropin_costs(torch, sd, h32):
+    """What an unchanged Rust caller of the reference pays (not the headline),
+    on cfg2's taps: the FIRFilter<f64, Complex<f64>> reference-typed EXACT device path, the
+    PCIe-inclusive host-slice execute_block, and per-sample Filter::execute latency."""
+    from solid_dsp_amd import FIRFilter
+    st = torch.cuda.current_stream()
+    out = {}
+    # (a) FIRFilter<f64, Complex<f64>> on the device, EXACT (bit-identical to the reference)
+    n = 1 << 26
+    f = FIRFilter(h32.astype(np.float64), 0.2, sample_dtype=np.complex128, algo=sd.ALGO_EXACT)
+    xi = torch.empty(2 * n, dtype=torch.float32, device="cuda")
+    sd.lib().sdsp_synth_f32_device(xi.data_ptr(), SEED, 0, 0, 2 * n, st.cuda_stream)
+    d_in = torch.view_as_complex(xi.view(-1, 2).to(torch.float64))
+    d_out = torch.empty_like(d_in)
+    f.execute_block_device(d_in, n, d_out, st)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        f.execute_block_device(d_in, n, d_out, st)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 3
+    out["f64_exact_device"] = {"Msamples_per_s": round(n / dt / 1e6, 1), "ms_per_2^26": round(dt * 1e3, 3),
+                               "GBps": round(32 * n / dt / 1e9, 1), "kernel": "fir_direct_kernel<double, c64, EXACT>"}
+    del xi, d_in, d_out
+    # (b) host slices through execute_block (H2D + kernel + D2H, pageable numpy buffers)
+    for name, dtype, algo, m in [("host_slice_c32_fft", np.complex64, sd.ALGO_FFT, 1 << 25),
+                                 ("host_slice_f64_exact", np.complex128, sd.ALGO_EXACT, 1 << 24)]:
+        g = FIRFilter(h32.astype(np.float64) if dtype == np.complex128 else h32,
+                      0.2 if dtype == np.complex128 else np.float32(0.2), sample_dtype=dtype, algo=algo)
+        x = (np.random.default_rng(0).standard_normal(2 * m).astype(np.float32)).view(np.complex64).astype(dtype)
+        g.execute_block(x[:4096])
+        t0 = time.perf_counter()
+        g.execute_block(x)
+        dt = time.perf_counter() - t0
+        out[name] = {"Msamples_per_s": round(m / dt / 1e6, 1), "samples": m,
+                     "note": "PCIe-inclusive: host slice in, host Vec out (pageable buffers)"}
+    # (c) per-sample Filter::execute (one launch + one sync, output in host-mapped memory)
+    g = FIRFilter(h32.astype(np.float64), 0.2, sample_dtype=np.complex128)
+    for _ in range(50):
+        g.execute(0.5 + 0.25j)
+    k = 2000
+    t0 = time.perf_counter()
+    for _ in range(k):
+        g.execute(0.5 + 0.25j)
+    dt = (time.perf_counter() - t0) / k
+    out["per_sample_execute"] = {"us_per_call": round(dt * 1e6, 2), "calls": k,
+                                 "note": "FIRFilter<f64, Complex<f64>>::execute via the Python binding (ctypes adds ~1-2 us)"}
+    one = np.array([0.5 + 0.25j])
+    t0 = time.perf_counter()
+    for _ in range(k):
+        g.execute_block(one)
+    dt = (time.perf_counter() - t0) / k
+    out["per_sample_execute_block_n1"] = {"us_per_call": round(dt * 1e6, 2), "calls": k,
+                                          "note": "execute_block with one sample: H2D + kernel + history + D2H + sync"}
+    return out
+
+
 WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT, 9: Cfg9AGC,
              10: Cfg10Interp}
 # bounded CPU samples: about 10-20 s of single-thread work each on a current x86 host
@@ -889,6 +947,8 @@ def main():
                        "value": parity, "tolerance": tol, "ok": parity_ok},
             "gather": gather,
         }
+        if args.config == 2 and not args.no_dropin:
+            out["dropin"] = dropin_costs(torch, sd, w.h)
         if not args.no_cpu:
             cb = w.cpu(args.cpu_samples or CPU_DEFAULT[args.config])
             cb["host_nproc"] = os.cpu_count()

@@ -96,6 +96,8 @@ struct sdsp_fir {
     hipStream_t stream = nullptr;
     mutable StreamFence fence;         // last stream an execute call was queued on
     DevBuf stage_in, stage_out;
+    HostMapped step_out;  // per-sample execute: output at [0, 16), completion flag at [16, 20)
+    unsigned step_seq = 0;
     // overlap-save plan
     bool ols_ok = false;
     int ols_kernel = kOlsOneShot;  // SDSP_TUNE_OLS_KERNEL
@@ -494,9 +496,34 @@ int sdsp_fir_execute_block(sdsp_fir* h, const void* in, size_t n, void* out, siz
     return SDSP_OK;
 }
 
+namespace {
+// one input through the single-launch step kernel (kern_fir_step.hip): the
+// delay line shifts on the device, the output (when the phase emits and
+// `want` is set) lands in host-mapped memory -- one launch, one sync, no copies
+int fir_step(sdsp_fir* h, const void* sample, void* out, size_t* n_out, bool want) {
+    if (!h || !sample || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
+    SDSP_TRY(h->step_out.ensure(32), "alloc mapped output");
+    const bool emit = want && (h->M == 1 || (h->M - 1 - h->ci) % h->M == 0);  // decim.rs:221-231
+    unsigned* flag_h = reinterpret_cast<unsigned*>((char*)h->step_out.host + 16);
+    const unsigned seq = ++h->step_seq;
+    FirStepArgs a{sample, h->d_hist[h->cur].p, h->d_hist[h->cur ^ 1].p, h->d_taps_rev.p, h->scale.data(),
+                  h->step_out.dev, reinterpret_cast<unsigned*>((char*)h->step_out.dev + 16), seq, (int)h->L - 1,
+                  (int)h->L, emit, h->algo != SDSP_ALGO_FMA};
+    SDSP_TRY(launch_fir_step(h->dtype, a, h->stream), "fir step");
+    h->cur ^= 1;
+    h->ci = (h->ci + 1) % h->M;
+    SDSP_TRY(wait_host_flag(flag_h, seq, h->stream), "fir step wait");
+    if (emit && out) std::memcpy(out, h->step_out.host, sample_bytes(h->dtype));
+    if (n_out) *n_out = emit ? 1 : 0;
+    return SDSP_OK;
+}
+}  // namespace
+
 int sdsp_fir_execute(sdsp_fir* h, const void* sample, void* out, size_t* n_out) {
-    if (!h || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
-    return sdsp_fir_execute_block(h, sample, 1, out, n_out);
+    if (!out) return SDSP_E_INVALID_ARGUMENT;
+    return fir_step(h, sample, out, n_out, true);
 }
 
 int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n) {
@@ -516,7 +543,10 @@ int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n) {
     return SDSP_OK;
 }
 
-int sdsp_decim_push(sdsp_fir* h, const void* sample) { return sdsp_decim_write(h, sample, 1); }
+int sdsp_decim_push(sdsp_fir* h, const void* sample) {
+    if (h && h->channels != 1) return sdsp_decim_write(h, sample, 1);  // one sample per channel
+    return fir_step(h, sample, nullptr, nullptr, false);
+}
 
 int sdsp_fir_reset(sdsp_fir* h) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;

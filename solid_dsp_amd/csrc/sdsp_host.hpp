@@ -47,6 +47,41 @@ inline cd coef_at(const unsigned char* p, int dt, size_t i) {
 }
 
 // owned device allocation
+// pinned host memory mapped into the device address space (coherent): a kernel
+// writes it directly, the host reads it after the stream synchronises
+struct HostMapped {
+    void* host = nullptr;
+    void* dev = nullptr;
+    HostMapped() = default;
+    HostMapped(const HostMapped&) = delete;
+    HostMapped& operator=(const HostMapped&) = delete;
+    ~HostMapped() {
+        if (host) (void)hipHostFree(host);
+    }
+    hipError_t ensure(size_t bytes) {
+        if (host) return hipSuccess;
+        hipError_t e = hipHostMalloc(&host, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess) {
+            host = nullptr;
+            return e;
+        }
+        return hipHostGetDevicePointer(&dev, host, 0);
+    }
+};
+
+// Wait until a kernel has released *flag == seq into host-mapped memory: a short
+// spin (the step kernels finish within microseconds of the launch), then the
+// stream's own synchronisation, which also surfaces launch errors.
+inline hipError_t wait_host_flag(const unsigned* flag, unsigned seq, hipStream_t s) {
+    for (int i = 0; i < (1 << 22); ++i) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return hipSuccess;
+        __builtin_ia32_pause();
+    }
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq ? hipSuccess : hipErrorUnknown;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;

@@ -68,6 +68,23 @@ struct PfbArgs {
 };
 hipError_t launch_pfb(int dtype, const PfbArgs& a, hipStream_t s);
 
+// one-sample FIR step (kern_fir_step.hip): shifts the delay line (last Lm1 of
+// hist_in + sample -> hist_out), if emit writes one output to `out`, then
+// releases *flag = seq (both host-mapped); the sample is passed by value
+struct FirStepArgs {
+    const void* sample;  // host pointer, copied into the launch
+    const void* hist_in;
+    void* hist_out;
+    const void* taps_rev;
+    const void* scale;  // host pointer to one Coef
+    void* out;
+    unsigned* flag;
+    unsigned seq;
+    int Lm1, L;
+    bool emit, exact;
+};
+hipError_t launch_fir_step(int dtype, const FirStepArgs& a, hipStream_t s);
+
 // IIR: SOS cascade (sections > 0) or Normal DF-II (sections == 0)
 struct IirArgs {
     const void* x;
