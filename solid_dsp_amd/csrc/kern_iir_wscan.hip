@@ -100,11 +100,17 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
     return v;
 }
 
+// Rate changes (DecimatingIIRFilter decim.rs:221-231, InterpolatingIIRFilter
+// interp.rs:204-210): the scan runs at the domain rate (nd = n Mi samples).  With
+// Mi > 1 the staged domain sample k is x[k / Mi] at k % Mi == 0, else zero; with
+// Md > 1 only domain samples k = j0 + o Md are stored, as y[o] (gathered from the
+// slab so that 64 consecutive outputs leave per store instruction).
 template <int S, typename C, typename I, int CB, bool RERUN>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
-                 const I* __restrict__ st_in, I* __restrict__ st_out, long long nd, int wc, int tpw, bool vec_ok) {
+                 const I* __restrict__ st_in, I* __restrict__ st_out, long long nd, int wc, int tpw, bool vec_ok,
+                 int Mi, int Md, long long j0, long long nout) {
     constexpr int D = 2 * S;
     constexpr int B = ws_chunk<I, CB>::B;
     constexpr int E = 16 / (int)sizeof(I);  // samples per 16-byte vector
@@ -122,10 +128,16 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     __syncthreads();
 
     const int ch = blockIdx.y;
-    x += (long long)ch * nd;
-    y += (long long)ch * nd;
+    x += (long long)ch * (nd / Mi);
+    y += (long long)ch * nout;
     st_in += (long long)ch * D;
     st_out += (long long)ch * D;
+    // domain sample k (zero outside the call)
+    auto dom = [&](long long k) -> I {
+        if (k < 0 || k >= nd) return zero_v<I>();
+        if (Mi == 1) return x[k];
+        return k % Mi == 0 ? x[k / Mi] : zero_v<I>();
+    };
 
     const long long gw = (long long)blockIdx.x * kWsWaves + wave;  // wave's segment
     const long long segc = (long long)tpw * 64 - wc;                  // chunks per segment
@@ -139,7 +151,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 
     // interior tiles are read with straight-line 16-byte loads, one tile ahead of
     // the compute (a per-vector branch would serialise the HBM round trips)
-    auto interior_at = [&](long long k0) { return vec_ok && k0 >= 0 && k0 + 64LL * B <= nd; };
+    auto interior_at = [&](long long k0) { return vec_ok && Mi == 1 && k0 >= 0 && k0 + 64LL * B <= nd; };
     v4u pre[kVecPerRow];
     {
         const long long k0 = (c_lo - wc) * B;
@@ -168,7 +180,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 const long long kv = k0 + (long long)v * E;
                 I tmp[E];
 #pragma unroll
-                for (int e = 0; e < E; ++e) tmp[e] = (kv + e >= 0 && kv + e < nd) ? x[kv + e] : zero_v<I>();
+                for (int e = 0; e < E; ++e) tmp[e] = dom(kv + e);
                 *reinterpret_cast<v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16) = to_v4<I>(tmp);
             }
         }
@@ -271,14 +283,26 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             I w1[S], w2[S];
 #pragma unroll
             for (int q = 0; q < S; ++q) { w1[q] = init[2 * q]; w2[q] = init[2 * q + 1]; }
-            for (long long k = kc; k < nd; ++k) (void)sos_step_f<S>(coefs, x[k], w1, w2);
+            for (long long k = kc; k < nd; ++k) (void)sos_step_f<S>(coefs, dom(k), w1, w2);
 #pragma unroll
             for (int q = 0; q < S; ++q) { st_out[2 * q] = w1[q]; st_out[2 * q + 1] = w2[q]; }
         }
         wave_sync();
 
         // 5. coalesced store of the segment's samples
-        if (interior && k0 >= k_lo) {
+        if (Md > 1) {  // decimated: outputs o with domain index j0 + o Md inside this tile's share
+            const long long ka = k0 > k_lo ? k0 : k_lo;
+            const long long kb = k0 + 64LL * B < nd ? k0 + 64LL * B : nd;
+            if (kb > ka && kb > j0) {
+                const long long oa = ka <= j0 ? 0 : (ka - j0 + Md - 1) / Md;
+                const long long ob = (kb - 1 - j0) / Md + 1;  // exclusive
+                for (long long o = oa + lane; o < ob; o += 64) {
+                    const int pos = (int)(j0 + o * Md - k0), v = pos / E;
+                    y[o] = *reinterpret_cast<const I*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16 +
+                                                       (pos % E) * (int)sizeof(I));
+                }
+            }
+        } else if (interior && k0 >= k_lo) {
 #pragma unroll
             for (int j = 0; j < kVecPerRow; ++j) {
                 const int v = lane + 64 * j;
@@ -596,7 +620,7 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
 template <typename C, typename I, int S, int CB, bool RERUN>
 hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     constexpr int B = ws_chunk<I, CB>::B;
-    const long long nd = (long long)a.n;
+    const long long nd = (long long)a.n * a.Mi;  // domain samples
     const long long nch = (nd + B - 1) / B;
     // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
     int tpw = (int)(nch / (64LL * 4096));
@@ -608,9 +632,10 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
                         (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
     const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * 4 * S * S + B * 2 * S);
+    const long long j0 = a.Md > 1 ? (long long)((a.Md - 1 - a.phase) % a.Md) : 0;  // first emitting domain index
     hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
-                       tpw, vec_ok);
+                       tpw, vec_ok, a.Mi, a.Md, j0, a.Md > 1 ? (long long)a.nout : nd);
     return hipGetLastError();
 }
 
@@ -631,6 +656,8 @@ hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
 
 template <typename C, typename I>
 hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
+    if (a.Mi != 1 || a.Md != 1)  // rate changes: the single-chunk kernels only
+        return a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st) : launch_wscan_s<C, I, 256>(a, st);
     if constexpr (std::is_same<I, float>::value) {
         if (a.ws_variant == 2) return launch_wscan2_s<128>(a, st);
         if (a.ws_variant == 3) return launch_wscan2_s<64>(a, st);

@@ -482,8 +482,9 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
             IirArgs a{src, dst, (const unsigned char*)h->d_coefs.p + 5 * gr.first * cb, gr.d_P.p,
                       st_in + soff, st_out + soff, n_g, last ? nout : nd, h->channels, gr.count, 0, 0, 0,
                       first ? Mi : 1, last ? Md : 1, last ? h->phase : 0, group_scan(h, gr, nd), gr.wc};
-            const int wv = h->wscan - 1;
-            if (a.algo_scan && a.Mi == 1 && a.Md == 1 && wv >= 0 && gr.ws[wv].wc > 0) {
+            int wv = h->wscan - 1;
+            if ((a.Mi != 1 || a.Md != 1) && (wv == 2 || wv == 3)) wv = 0;  // paired kernels: no rate changes
+            if (a.algo_scan && wv >= 0 && gr.ws[wv].wc > 0) {
                 a.P = gr.ws[wv].d_P.p;
                 a.Cr = gr.ws[wv].d_Cr.p;
                 a.wc = gr.ws[wv].wc;

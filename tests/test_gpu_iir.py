@@ -278,3 +278,45 @@ def test_get_set_state_roundtrip():
     g = IIRFilter(ff, fb, SO, sample_dtype=np.float64, algo=sd.ALGO_EXACT)
     g.set_state(st, ph)
     assert bits_equal(f.execute_block(x[10000:]), g.execute_block(x[10000:]))
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", [(O.RR32, np.float32, np.float32), (O.RC32, np.float32, np.complex64),
+                                        (O.RR64, np.float64, np.float64), (O.RC64, np.float64, np.complex128)])
+@pytest.mark.parametrize("M", [2, 7, 32])
+def test_wave_scan_rate_changes_ragged(dt, cdt, sdt, M):
+    """decimating / interpolating SOS cascades on the wave scan (kern_iir_wscan.hip, Mi/Md paths):
+    ragged calls so the decimation phase and the interpolated tiles straddle every boundary"""
+    ff, fb = butter()
+    ff, fb = ff.astype(cdt), fb.astype(cdt)
+    rng = np.random.default_rng(M + dt)
+    n = 150001
+    x = (rng.standard_normal(n) + (1j * rng.standard_normal(n) if np.dtype(sdt).kind == "c" else 0)).astype(sdt)
+    tol = 1e-5 if cdt == np.float32 else 1e-12
+    ref_dt = O.RC64 if np.dtype(sdt).kind == "c" else O.RR64
+    x64 = x.astype(np.complex128 if np.dtype(sdt).kind == "c" else np.float64)
+    cuts = [0, 1, 4097, 33333, 100000, n]
+    f = DecimatingIIRFilter(ff, fb, SO, M, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(cuts, cuts[1:])])
+    ref = O.iir_decim(ref_dt, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER, M).execute_block(x64)
+    assert len(y) == len(ref) and rel_rms(y, ref) <= tol
+    m = 40000
+    g = InterpolatingIIRFilter(ff, fb, SO, M, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    y = np.concatenate([g.execute_block(x[a:b]) for a, b in zip([0, 3, 9000], [3, 9000, m])])
+    ref = O.iir_interp(ref_dt, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER, M).execute_block(x64[:m])
+    assert len(y) == len(ref) and rel_rms(y, ref) <= tol
+
+
+def test_wave_scan_decim_multichannel_device():
+    import torch
+    ff, fb = butter()
+    ch, n, M = 3, 70001, 4
+    x = np.stack([O.synth(5, c, 0, n) for c in range(ch)]).astype(np.float32)
+    f = DecimatingIIRFilter(ff.astype(np.float32), fb.astype(np.float32), SO, M, sample_dtype=np.float32,
+                            algo=sd.ALGO_FMA, channels=ch)
+    nout = f.output_count(n)
+    d_out = torch.empty(ch * nout, dtype=torch.float32, device="cuda")
+    f.execute_block_device(torch.from_numpy(x.reshape(-1)).cuda(), n, d_out, torch.cuda.current_stream())
+    y = d_out.cpu().numpy().reshape(ch, nout)
+    for c in range(ch):
+        ref = O.iir_decim(O.RR64, ff, fb, O.SECOND_ORDER, M).execute_block(x[c].astype(np.float64))
+        assert rel_rms(y[c], ref) <= 1e-5
