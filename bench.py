@@ -18,6 +18,7 @@ SURVEY §8f rows (build-defined cases, same parity + measurement fields):
   8  batched 2^20-point forward FFT (four-step), c32, 2^28 samples
   9  AGC bank, Complex<f64>, 2^18 channels x 2^10 samples
  10  32x interpolating FIR (K = 8), crcf, 2^25 inputs -> 2^30 outputs
+ 11  IIRFilter<f64, Complex<f64>> active_lag bank (the reference demo's filter), 2^16 channels x 2^12
 
 With N ranks each rank processes its own independent channel(s) (weak
 scaling, no collective in the timed region); RCCL is used afterwards only for
@@ -50,7 +51,7 @@ def parse():
                    help="ranks (one per GPU); outside torch.distributed.run this process spawns them itself")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, default=2, choices=list(range(1, 11)))
+    p.add_argument("--config", type=int, default=2, choices=list(range(1, 12)))
     p.add_argument("--log2n", type=int, default=30, help="samples per GPU per step (configs 2-4)")
     p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"], help="config 2 kernel")
     p.add_argument("--cpu-samples", type=int, default=None,
@@ -769,11 +770,66 @@ def dropin_costs(torch, sd, h32):
     return out
 
 
+class Cfg11ActiveLag:
+    """A bank of IIRFilter<f64, Complex<f64>> SecondOrder on the reference demo's active_lag(0.02,
+    1/sqrt 2, 1000) PLL loop filter (src/main.rs:37-40, iirdes/pll/mod.rs:24-99): 2^16 channels x
+    2^12 samples, the reference-order serial recurrence (one lane per channel, bit-identical).  The
+    cascade integrates its input, so no block-parallel scan applies (DESIGN.md §4 IIR)."""
+    metric = "Msamples/sec IIRFilter<f64, Complex<f64>> active_lag bank, reference-order (bit-exact); % HBM roofline"
+    tol = 0
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import IIRFilter, IIRFilterType
+        from solid_dsp_amd.filter import iirdes
+        self.num, self.den = iirdes.pll.active_lag(0.02, 1.0 / np.sqrt(2.0), 1000.0)
+        self.ch, self.n = 1 << 16, 1 << 12
+        self.make = lambda d=dev: IIRFilter(self.num, self.den, IIRFilterType.SecondOrder, sample_dtype=np.complex128,
+                                            device=d, channels=self.ch, algo=sd.ALGO_EXACT)
+        self.f = self.make()
+        total = self.ch * self.n
+        tmp = torch.empty(2 * total, dtype=torch.float32, device="cuda")
+        sd.lib().sdsp_synth_f32_device(tmp.data_ptr(), SEED, rank, 0, 2 * total, torch.cuda.current_stream().cuda_stream)
+        self.d_in = torch.view_as_complex(tmp.view(-1, 2).to(torch.float64)).contiguous()
+        del tmp
+        self.d_out = torch.empty_like(self.d_in)
+        self.samples_per_step = total
+        self.bytes_per_step = 32 * total
+        self.dtype = "c64 (f64 coefficients, Complex<f64> samples, reference summation order)"
+        self.kernel = "sos_serial_kernel<1, double, c64> (one lane per channel)"
+        self.parity_check = "bit mismatches vs the f64 restatement over 16 channels (must be 0)"
+        self.workload = "cfg11: active_lag IIRFilter<f64, Complex<f64>> bank, 2^16 channels x 2^12 samples"
+        self.algo_name = "iir_serial_bank"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng):
+        import oracle_lib as O
+        import torch
+        g = self.make()
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        bad = 0
+        for c in range(16):
+            x = self.d_in[c * self.n:(c + 1) * self.n].cpu().numpy()
+            y = self.d_out[c * self.n:(c + 1) * self.n].cpu().numpy()
+            ref = O.iir(O.RC64, self.num, self.den, O.SECOND_ORDER).execute_block(x)
+            bad += int(np.count_nonzero(y.view(np.uint64) != ref.view(np.uint64)))
+        return float(bad)
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = O.synth(SEED, 0, 0, CPU_CHUNK, complex_=True).astype(np.complex128)
+        f = O.iir(O.RC64, self.num, self.den, O.SECOND_ORDER)
+        return timed_cpu(lambda c: f.execute_block(x), "IIRFilter<f64, Complex<f64>> SecondOrder restatement "
+                         "(active_lag, one channel)", samples, CPU_CHUNK)
+
+
 WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT, 9: Cfg9AGC,
-             10: Cfg10Interp}
+             10: Cfg10Interp, 11: Cfg11ActiveLag}
 # bounded CPU samples: about 10-20 s of single-thread work each on a current x86 host
 CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 << 25, 7: 1 << 28, 8: 1 << 24, 9: 1 << 25,
-               10: 1 << 30}
+               10: 1 << 30, 11: 1 << 28}
 CPU_CHUNK = 1 << 22
 
 

@@ -251,6 +251,10 @@ SDSP_API int sdsp_iir_set_algo(sdsp_iir* h, int algo);
 SDSP_API int sdsp_iir_set_tuning(sdsp_iir* h, int key, int value);
 /* scan plan of section group g: warm-up chunks (0 = scan not admissible) and chunk length */
 SDSP_API int sdsp_iir_scan_info(const sdsp_iir* h, int group, int* warmup_chunks, int* chunk);
+/* the wave scan a cascade group gets when the scan is requested: 0 none (serial recurrence),
+ * 1 warm-up chunks (decaying state response), 2 exact inter-wave carries (non-decaying but
+ * well conditioned: aggregate pass + carry scan + output pass); -1 bad handle/group */
+SDSP_API int sdsp_iir_wscan_mode(const sdsp_iir* h, int group);
 SDSP_API size_t sdsp_iir_output_count(const sdsp_iir* h, size_t n);
 /* Filter::execute / execute_block                     mod.rs:270-316, decim.rs:203-225, interp.rs:197-214 */
 SDSP_API int sdsp_iir_execute(sdsp_iir* h, const void* sample, void* out, size_t* n_out);

@@ -113,6 +113,7 @@ def _declare(L):
         "sdsp_pfb_execute": (i, [vp, sz, vp]),
         "sdsp_pfb_reset": (i, [vp]),
         "sdsp_pfb_set_algo": (i, [vp, i]),
+        "sdsp_iir_wscan_mode": (i, [vp, i]),
         "sdsp_pfb_set_channels": (i, [vp, sz]),
         "sdsp_pfb_execute_block": (i, [vp, vp, sz, vp]),
         "sdsp_pfb_execute_block_device": (i, [vp, vp, sz, vp, vp]),

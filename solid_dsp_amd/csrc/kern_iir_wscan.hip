@@ -110,7 +110,8 @@ __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
                  const I* __restrict__ st_in, I* __restrict__ st_out, long long nd, int wc, int tpw, bool vec_ok,
-                 int Mi, int Md, long long j0, long long nout) {
+                 int Mi, int Md, long long j0, long long nout, const I* __restrict__ cin, I* __restrict__ gagg,
+                 long long nwaves) {
     constexpr int D = 2 * S;
     constexpr int B = ws_chunk<I, CB>::B;
     constexpr int E = 16 / (int)sizeof(I);  // samples per 16-byte vector
@@ -145,9 +146,12 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     const long long k_lo = c_lo * B;
     if (k_lo >= nd) return;
 
+    // carry entering the wave's first tile: zero (warm-up lanes settle it, wave 0 injects
+    // st_in), or the exact carry of the aggregate pass + carry scan (cin)
     I carry[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) carry[d] = zero_v<I>();
+    for (int d = 0; d < D; ++d) carry[d] = cin ? cin[((long long)ch * nwaves + gw) * D + d] : zero_v<I>();
+    const bool agg = gagg != nullptr;  // aggregate pass: the wave's zero-carry end state only
 
     // interior tiles are read with straight-line 16-byte loads, one tile ahead of
     // the compute (a per-vector branch would serialise the HBM round trips)
@@ -212,7 +216,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 #pragma unroll
             for (int q = 0; q < S; ++q) { s[2 * q] = w1[q]; s[2 * q + 1] = w2[q]; }
         }
-        if (gw == 0 && t == 0 && lane == wc - 1) {  // the call's exact carried state enters here
+        if (!cin && !agg && gw == 0 && t == 0 && lane == wc - 1) {  // the call's exact carried state enters here
 #pragma unroll
             for (int d = 0; d < D; ++d) s[d] = st_in[d];
         }
@@ -245,6 +249,10 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         }
 #pragma unroll
         for (int d = 0; d < D; ++d) carry[d] = readlane_v(s[d], 63);
+        if (agg) {
+            wave_sync();
+            continue;
+        }
 
         // 4. outputs: correction by the state response (y0 in place), or (RERUN) the
         //    chunk rerun from its true initial state over the staged input
@@ -323,6 +331,107 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             }
         }
         wave_sync();
+    }
+    if (agg && lane == 0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) gagg[((long long)ch * nwaves + gw) * D + d] = carry[d];
+    }
+}
+
+// Exact carries between the waves of one channel (one workgroup per channel):
+// cin[0] = st_in, cin[w + 1] = Phi cin[w] + G[w].  Each of the 256 lanes folds a
+// contiguous run of R waves (Horner with Phi), lane 0 chains the 256 run
+// aggregates with Phi^R, then every lane replays its run from its exact prefix.
+template <int D, typename C, typename I>
+__device__ __forceinline__ void matvec_full(const C* __restrict__ P, const I (&x)[D], I (&y)[D]) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        I acc = mul_(P[r * D], x[0]);
+#pragma unroll
+        for (int c = 1; c < D; ++c) acc = fmac_(acc, P[r * D + c], x[c]);
+        y[r] = acc;
+    }
+}
+
+template <int D, typename C, typename I>
+__global__ void __launch_bounds__(256)
+wscan_carry_kernel(const I* __restrict__ G, I* __restrict__ cin, const C* __restrict__ Phi, const I* __restrict__ st_in,
+                   long long W) {
+    __shared__ C sPhi[D * D], sPhiR[D * D];
+    __shared__ I agg[256][D];
+    const int t = threadIdx.x, ch = blockIdx.x;
+    G += (long long)ch * W * D;
+    cin += (long long)ch * W * D;
+    st_in += (long long)ch * D;
+    const long long R = (W + 255) / 256;
+    if (t < D * D) sPhi[t] = Phi[t];
+    __syncthreads();
+    if (t == 0) {  // Phi^R by repeated squaring (R >= 1), in the Coef type
+        C acc[D * D], base[D * D], tmp[D * D];
+        for (int i = 0; i < D * D; ++i) { acc[i] = (i % (D + 1) == 0) ? C(1) : C(0); base[i] = sPhi[i]; }
+        for (long long e = R; e > 0; e >>= 1) {
+            if (e & 1) {
+                for (int i = 0; i < D; ++i)
+                    for (int j = 0; j < D; ++j) {
+                        C v = C(0);
+                        for (int k = 0; k < D; ++k) v = fmac_(v, acc[i * D + k], base[k * D + j]);
+                        tmp[i * D + j] = v;
+                    }
+                for (int i = 0; i < D * D; ++i) acc[i] = tmp[i];
+            }
+            for (int i = 0; i < D; ++i)
+                for (int j = 0; j < D; ++j) {
+                    C v = C(0);
+                    for (int k = 0; k < D; ++k) v = fmac_(v, base[i * D + k], base[k * D + j]);
+                    tmp[i * D + j] = v;
+                }
+            for (int i = 0; i < D * D; ++i) base[i] = tmp[i];
+        }
+        for (int i = 0; i < D * D; ++i) sPhiR[i] = acc[i];
+    }
+    const long long w0 = (long long)t * R, w1 = w0 + R < W ? w0 + R : W;
+    I a[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) a[d] = zero_v<I>();
+    for (long long w = w0; w < w1; ++w) {  // a = Phi a + G[w]
+        I b[D];
+        matvec_full<D>(sPhi, a, b);
+#pragma unroll
+        for (int d = 0; d < D; ++d) a[d] = add_(b[d], G[w * D + d]);
+    }
+    // a run shorter than R (the tail) is padded with zero aggregates at its front so
+    // that every run spans R waves: only the last non-empty run can be short, and its
+    // aggregate is not needed by any later run
+#pragma unroll
+    for (int d = 0; d < D; ++d) agg[t][d] = a[d];
+    __syncthreads();
+    if (t == 0) {  // exclusive prefixes over runs: p_{j+1} = Phi^R p_j + agg_j
+        I p[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) p[d] = st_in[d];
+        for (int j = 0; j < 256; ++j) {
+            I q[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) q[d] = agg[j][d];
+#pragma unroll
+            for (int d = 0; d < D; ++d) agg[j][d] = p[d];
+            I b[D];
+            matvec_full<D>(sPhiR, p, b);
+#pragma unroll
+            for (int d = 0; d < D; ++d) p[d] = add_(b[d], q[d]);
+        }
+    }
+    __syncthreads();
+    I c[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) c[d] = agg[t][d];
+    for (long long w = w0; w < w1; ++w) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) cin[w * D + d] = c[d];
+        I b[D];
+        matvec_full<D>(sPhi, c, b);
+#pragma unroll
+        for (int d = 0; d < D; ++d) c[d] = add_(b[d], G[w * D + d]);
     }
 }
 
@@ -617,25 +726,42 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+template <int CB> int wscan_tpw(long long nch) {
+    // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
+    int tpw = (int)(nch / (64LL * 4096));
+    return tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
+}
+
 template <typename C, typename I, int S, int CB, bool RERUN>
 hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     constexpr int B = ws_chunk<I, CB>::B;
+    constexpr int D = 2 * S;
     const long long nd = (long long)a.n * a.Mi;  // domain samples
     const long long nch = (nd + B - 1) / B;
-    // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
-    int tpw = (int)(nch / (64LL * 4096));
-    tpw = tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
+    const int tpw = wscan_tpw<CB>(nch);
     const long long segc = (long long)tpw * 64 - a.wc;
     const long long waves = (nch + segc - 1) / segc;
+    const bool exact = a.wc == 0;  // exact inter-wave carries: aggregate pass + carry scan first
+    if (exact && (!a.Phi || !a.G || !a.Cin || (size_t)waves > a.scratch_waves)) return hipErrorInvalidValue;
     dim3 grid((unsigned)((waves + kWsWaves - 1) / kWsWaves), (unsigned)a.channels);
     // 16-byte vector path: aligned bases and channel strides
     const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
                         (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
     const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * 4 * S * S + B * 2 * S);
     const long long j0 = a.Md > 1 ? (long long)((a.Md - 1 - a.phase) % a.Md) : 0;  // first emitting domain index
+    const long long ny = a.Md > 1 ? (long long)a.nout : nd;
+    if (exact) {
+        hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
+                           (I*)a.y, (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out,
+                           nd, 0, tpw, vec_ok, a.Mi, a.Md, j0, ny, (const I*)nullptr, (I*)a.G, waves);
+        hipLaunchKernelGGL((wscan_carry_kernel<D, C, I>), dim3((unsigned)a.channels), dim3(256), 0, st,
+                           (const I*)a.G, (I*)a.Cin, (const C*)a.Phi + (size_t)(tpw - 1) * D * D, (const I*)a.st_in,
+                           waves);
+    }
     hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
-                       tpw, vec_ok, a.Mi, a.Md, j0, a.Md > 1 ? (long long)a.nout : nd);
+                       tpw, vec_ok, a.Mi, a.Md, j0, ny, exact ? (const I*)a.Cin : (const I*)nullptr, (I*)nullptr,
+                       waves);
     return hipGetLastError();
 }
 
@@ -656,7 +782,7 @@ hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
 
 template <typename C, typename I>
 hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
-    if (a.Mi != 1 || a.Md != 1)  // rate changes: the single-chunk kernels only
+    if (a.Mi != 1 || a.Md != 1 || a.wc == 0)  // rate changes / exact carries: the single-chunk kernels only
         return a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st) : launch_wscan_s<C, I, 256>(a, st);
     if constexpr (std::is_same<I, float>::value) {
         if (a.ws_variant == 2) return launch_wscan2_s<128>(a, st);
@@ -667,6 +793,15 @@ hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
 }
 
 }  // namespace
+
+size_t iir_wscan_waves(int dtype, const IirArgs& a) {
+    const int B = iir_wscan_chunk(dtype, a.ws_variant == 1 ? 1 : 0);
+    if (B == 0) return 0;
+    const long long nch = ((long long)a.n * a.Mi + B - 1) / B;
+    const int tpw = a.ws_variant == 1 ? wscan_tpw<128>(nch) : wscan_tpw<256>(nch);
+    const long long segc = (long long)tpw * 64 - a.wc;
+    return (size_t)((nch + segc - 1) / segc);
+}
 
 int iir_wscan_chunk(int dtype, int variant) {
     // variants: 0 = 256-byte chunks, 1 = 128-byte, 2/3 = paired 128/64-byte chunks (real f32 only),

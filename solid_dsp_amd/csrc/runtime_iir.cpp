@@ -36,7 +36,9 @@ struct Group {
     DevBuf d_P;                // [8][2c][2c]
     struct WaveScan {          // wave-scan tables per chunk-size variant (256 B, 128 B)
         int wc = 0;
+        bool exact = false;    // wc == 0 but bounded: exact inter-wave carries (Phi)
         DevBuf d_P, d_Cr;      // [6][2c][2c], [B][2c] output response to the state
+        DevBuf d_Phi;          // exact carries: [8][2c][2c] A^(64 B t), t = 1..8
     } ws[5];
 };
 
@@ -98,7 +100,7 @@ struct sdsp_iir {
     std::vector<unsigned char> cdev;     // normalised coefficients in the Coef type (device layout)
     int S = 0, nb = 0, na = 0, cap = 0;
     std::vector<Group> groups;
-    DevBuf d_coefs, d_state[2], d_tmp[2];
+    DevBuf d_coefs, d_state[2], d_tmp[2], d_carry[2];
     int cur = 0;
     int algo = SDSP_ALGO_EXACT;  // reference-order recurrence unless the caller opts in (sdsp.h)
     int wscan = 1;  // 0: block scan; 1-4: wave-scan variant 0-3 (kern_iir_wscan.hip; sdsp_iir_set_tuning)
@@ -162,11 +164,70 @@ Mat sos_A(const sdsp_iir* h, int first, int count) {
     return A;
 }
 
+// run sections [first, first+count) over x from state s (in place), f64
+void sos_run(const sdsp_iir* h, const Group& g, const double* x, double* y, size_t n, std::vector<double>& s) {
+    for (size_t i = 0; i < n; ++i) {
+        double v = x[i];
+        for (int q = 0; q < g.count; ++q) {
+            const double* c = &h->c64[5 * (g.first + q)];
+            const double w = v - (c[3] * s[2 * q] + c[4] * s[2 * q + 1]);
+            v = c[0] * w + c[1] * s[2 * q] + c[2] * s[2 * q + 1];
+            s[2 * q + 1] = s[2 * q];
+            s[2 * q] = w;
+        }
+        if (y) y[i] = v;
+    }
+}
+
+// Is carrying chunk states through A^B as accurate as the recurrence itself?  A
+// cascade that integrates its input (e.g. active_lag: poles at 1 and 1 - 1.6e-6)
+// grows states ~1e6 x its output, and re-associating the recurrence through
+// powers of A then loses 3-6 digits against the reference-order loop (measured:
+// 8e-6 relative at 2^18 samples, against 2e-9 for the serial f64 loop).  A host
+// probe in f64 -- zero-state chunks corrected by exactly carried states, against
+// the serial loop over 2^14 pseudo-random samples -- admits the exact-carry scan
+// only when the two agree to 1e-11.
+bool carry_well_conditioned(const sdsp_iir* h, const Group& g, int B, const Mat& AB) {
+    const int D = 2 * g.count;
+    const size_t n = 1 << 14;
+    std::vector<double> x(n), ys(n), yc(n);
+    uint64_t r = 0x9E3779B97F4A7C15ULL;
+    for (auto& v : x) {
+        r = r * 6364136223846793005ULL + 1442695040888963407ULL;
+        v = (double)(r >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+    }
+    std::vector<double> st(D, 0.0);
+    sos_run(h, g, x.data(), ys.data(), n, st);
+    std::vector<double> I(D, 0.0), e(D), cr(D * (size_t)B);
+    for (int d = 0; d < D; ++d) {  // Cr[i][d]: output response to basis state e_d
+        std::vector<double> zs(D, 0.0), zero(B, 0.0), out(B);
+        zs[d] = 1.0;
+        sos_run(h, g, zero.data(), out.data(), B, zs);
+        for (int i = 0; i < B; ++i) cr[(size_t)i * D + d] = out[i];
+    }
+    for (size_t k = 0; k < n; k += B) {
+        std::fill(e.begin(), e.end(), 0.0);
+        sos_run(h, g, &x[k], &yc[k], B, e);
+        for (int i = 0; i < B; ++i)
+            for (int d = 0; d < D; ++d) yc[k + i] += cr[(size_t)i * D + d] * I[d];
+        std::vector<double> nI(D, 0.0);
+        for (int a = 0; a < D; ++a) {
+            for (int b = 0; b < D; ++b) nI[a] += AB[a * D + b] * I[b];
+            nI[a] += e[a];
+        }
+        I = nI;
+    }
+    double num = 0.0, den = 0.0;
+    for (size_t i = 0; i < n; ++i) { num += (yc[i] - ys[i]) * (yc[i] - ys[i]); den += ys[i] * ys[i]; }
+    return std::isfinite(num) && den > 0.0 && std::sqrt(num / den) <= 1e-11;
+}
+
 // Scan tables for chunks of B samples: warm-up chunks wc (smallest m with
 // ||A^(mB)||_inf < tol, m <= max_wc; 0 = the scan is not admissible), P_k =
 // A^(B 2^k) for k < nP, and optionally Cr[i][d] (i < B): the cascade output i
 // steps after starting from basis state e_d with zero input.
-int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, int* wc, DevBuf* dP, DevBuf* dCr) {
+int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, int* wc, DevBuf* dP, DevBuf* dCr,
+                DevBuf* dPhi = nullptr, bool* exact = nullptr) {
     const double tol = is_f32(h->dtype) ? 1e-9 : 1e-17;
     const int D = 2 * g.count;
     const Mat A = sos_A(h, g.first, g.count);
@@ -179,7 +240,26 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
         if (nrm < tol) { *wc = m; break; }
         Am = matmul(Am, AB, D);
     }
-    if (*wc == 0) return SDSP_OK;
+    if (exact) *exact = false;
+    if (*wc == 0) {
+        // a state response that does not die out (e.g. a pole at z = 1, the active_lag PLL
+        // filter): exact carries between waves instead of warm-up, provided the powers of A
+        // over the longest wave segment stay bounded
+        if (!exact || !dPhi) return SDSP_OK;
+        const Mat A64 = matpow(AB, 64, D);
+        Mat At = A64;
+        std::vector<unsigned char> Phi;
+        for (int t = 1; t <= 8; ++t) {
+            const double nrm = norm_inf(At, D);
+            if (!std::isfinite(nrm) || nrm > 1e6) return SDSP_OK;
+            for (double v : At) push_coef(Phi, v, h->dtype);
+            At = matmul(At, A64, D);
+        }
+        if (!carry_well_conditioned(h, g, B, AB)) return SDSP_OK;
+        IIR_TRY(dPhi->ensure(Phi.size()), "alloc Phi");
+        IIR_TRY(hipMemcpy(dPhi->p, Phi.data(), Phi.size(), hipMemcpyHostToDevice), "copy Phi");
+        *exact = true;
+    }
     std::vector<unsigned char> P;
     Mat Pk = AB;
     for (int k = 0; k < nP; ++k) {
@@ -223,12 +303,14 @@ int plan_groups(sdsp_iir* h) {
         // block scan (kern_iir.hip): 8 powers, warm-up up to half the block's lanes
         int st = scan_tables(h, g, iir_scan_chunk(h->dtype), kScanLanes / 2, 8, &g.wc, &g.d_P, nullptr);
         if (st) return st;
-        if (g.wc == 0) continue;
-        // wave scan (kern_iir_wscan.hip), one table set per chunk size: 6 powers, warm-up <= 32 chunks
+        // wave scan (kern_iir_wscan.hip), one table set per chunk size: 6 powers, warm-up <= 32
+        // chunks; without a decaying state response the single-chunk variants carry exactly
         for (int v = 0; v < 5; ++v) {
             const int Bw = iir_wscan_chunk(h->dtype, v);
             if (Bw == 0) continue;
-            st = scan_tables(h, g, Bw, 32, 7, &g.ws[v].wc, &g.ws[v].d_P, &g.ws[v].d_Cr);
+            if (g.wc == 0 && v != 0 && v != 1) continue;
+            st = scan_tables(h, g, Bw, 32, 7, &g.ws[v].wc, &g.ws[v].d_P, &g.ws[v].d_Cr, &g.ws[v].d_Phi,
+                             &g.ws[v].exact);
             if (st) return st;
         }
     }
@@ -332,8 +414,17 @@ int iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void
     return SDSP_OK;
 }
 
-bool group_scan(const sdsp_iir* h, const Group& g, size_t nd) {
-    if (h->type != 1 || g.wc == 0) return false;
+// wave-scan variant index for this group (-1: none applies)
+int group_wscan(const sdsp_iir* h, const Group& g, bool rate_change) {
+    int wv = h->wscan - 1;
+    if ((rate_change || g.wc == 0) && (wv == 2 || wv == 3)) wv = 0;  // paired kernels: decaying, no rate change
+    if (wv < 0) return -1;
+    return (g.ws[wv].wc > 0 || g.ws[wv].exact) ? wv : -1;
+}
+
+bool group_scan(const sdsp_iir* h, const Group& g, size_t nd, bool rate_change) {
+    if (h->type != 1) return false;
+    if (g.wc == 0 && group_wscan(h, g, rate_change) < 0) return false;
     if (h->algo == SDSP_ALGO_EXACT) return false;
     if (h->algo == SDSP_ALGO_AUTO && nd < 8192) return false;
     return true;
@@ -377,10 +468,10 @@ void sdsp_iir_destroy(sdsp_iir* h) {
             (void)hipStreamDestroy(h->stream);
         }
         h->d_coefs.release();
-        for (int i = 0; i < 2; ++i) { h->d_state[i].release(); h->d_tmp[i].release(); }
+        for (int i = 0; i < 2; ++i) { h->d_state[i].release(); h->d_tmp[i].release(); h->d_carry[i].release(); }
         for (auto& g : h->groups) {
             g.d_P.release();
-            for (auto& w : g.ws) { w.d_P.release(); w.d_Cr.release(); }
+            for (auto& w : g.ws) { w.d_P.release(); w.d_Cr.release(); w.d_Phi.release(); }
         }
         h->stage_in.release();
         h->stage_out.release();
@@ -438,6 +529,13 @@ int sdsp_iir_scan_info(const sdsp_iir* h, int group, int* warmup_chunks, int* ch
     return SDSP_OK;
 }
 
+int sdsp_iir_wscan_mode(const sdsp_iir* h, int group) {
+    if (!h || group < 0 || group >= (int)h->groups.size()) return -1;
+    const int wv = group_wscan(h, h->groups[group], false);
+    if (wv < 0) return 0;
+    return h->groups[group].ws[wv].wc > 0 ? 1 : 2;
+}
+
 size_t sdsp_iir_output_count(const sdsp_iir* h, size_t n) {
     if (!h) return 0;
     if (h->mode == 2) return n * h->M;
@@ -479,17 +577,30 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
             const bool first = gi == 0, last = gi + 1 == ng;
             void* dst = last ? d_out : h->d_tmp[gi & 1].p;
             const size_t n_g = first ? n : nd;
+            const bool rc = (first && Mi != 1) || (last && Md != 1);
             IirArgs a{src, dst, (const unsigned char*)h->d_coefs.p + 5 * gr.first * cb, gr.d_P.p,
                       st_in + soff, st_out + soff, n_g, last ? nout : nd, h->channels, gr.count, 0, 0, 0,
-                      first ? Mi : 1, last ? Md : 1, last ? h->phase : 0, group_scan(h, gr, nd), gr.wc};
-            int wv = h->wscan - 1;
-            if ((a.Mi != 1 || a.Md != 1) && (wv == 2 || wv == 3)) wv = 0;  // paired kernels: no rate changes
-            if (a.algo_scan && wv >= 0 && gr.ws[wv].wc > 0) {
+                      first ? Mi : 1, last ? Md : 1, last ? h->phase : 0, group_scan(h, gr, nd, rc), gr.wc};
+            const int wv = group_wscan(h, gr, rc);
+            if (a.algo_scan && wv >= 0) {
                 a.P = gr.ws[wv].d_P.p;
                 a.Cr = gr.ws[wv].d_Cr.p;
                 a.wc = gr.ws[wv].wc;
                 a.ws_variant = wv;
+                if (a.wc == 0) {  // exact inter-wave carries: scratch for the aggregate pass
+                    a.Phi = gr.ws[wv].d_Phi.p;
+                    const size_t W = iir_wscan_waves(h->dtype, a);
+                    const size_t bytes = h->channels * W * 2 * gr.count * sbytes;
+                    IIR_TRY(h->d_carry[0].ensure(bytes), "iir carry scratch");
+                    IIR_TRY(h->d_carry[1].ensure(bytes), "iir carry scratch");
+                    a.G = h->d_carry[0].p;
+                    a.Cin = h->d_carry[1].p;
+                    a.scratch_waves = W;
+                }
                 IIR_TRY(launch_iir_wscan(h->dtype, a, s), "iir sos wave scan");
+            } else if (a.algo_scan && gr.wc == 0) {  // block scan needs the decaying response
+                a.algo_scan = false;
+                IIR_TRY(launch_iir(h->dtype, a, s), "iir sos");
             } else {
                 IIR_TRY(launch_iir(h->dtype, a, s), "iir sos");
             }

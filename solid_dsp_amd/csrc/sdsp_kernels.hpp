@@ -101,10 +101,19 @@ struct IirArgs {
     int wc;              // warm-up chunks (scan)
     const void* Cr = nullptr;  // wave scan: [B][2S] output response to the state, c A^i (Coef type)
     int ws_variant = 0;        // wave scan chunk: 0 = 256 bytes, 1 = 128 bytes
+    // exact inter-wave carries (wc == 0: cascades whose state response does not decay):
+    // Phi[t-1] = A^(64 B t) (t = tiles per wave, 1..8), scratch G / Cin [channels][waves][2S]
+    const void* Phi = nullptr;
+    void* G = nullptr;
+    void* Cin = nullptr;
+    size_t scratch_waves = 0;  // capacity of G / Cin per channel
 };
+// waves the exact-carry wave scan launches for this call (sizes G / Cin)
+size_t iir_wscan_waves(int dtype, const IirArgs& a);
 hipError_t launch_iir(int dtype, const IirArgs& a, hipStream_t s);
 int iir_scan_chunk(int dtype);  // samples per lane chunk of the scan kernel
-// wave-level scan (kern_iir_wscan.hip): SOS, no decimation/interpolation, wc <= 32
+// wave-level scan (kern_iir_wscan.hip): SOS cascades, with rate changes; wc <= 32
+// warm-up chunks, or wc == 0 with Phi/G/Cin: aggregate pass, carry scan, output pass
 hipError_t launch_iir_wscan(int dtype, const IirArgs& a, hipStream_t s);
 int iir_wscan_chunk(int dtype, int variant);  // samples per lane chunk of the wave scan
 

@@ -100,6 +100,10 @@ class _IirBase:
         st = np.ascontiguousarray(state, dtype=self.sample_dtype)
         L.check(L.lib().sdsp_iir_set_state(self._h, L.ptr(st) if st.size else None, phase))
 
+    def wscan_mode(self, group: int = 0) -> int:
+        """0 serial recurrence, 1 wave scan with warm-up, 2 wave scan with exact carries"""
+        return int(L.lib().sdsp_iir_wscan_mode(self._h, group))
+
     def output_count(self, n):
         return int(L.lib().sdsp_iir_output_count(self._h, n))
 

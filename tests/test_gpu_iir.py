@@ -320,3 +320,54 @@ def test_wave_scan_decim_multichannel_device():
     for c in range(ch):
         ref = O.iir_decim(O.RR64, ff, fb, O.SECOND_ORDER, M).execute_block(x[c].astype(np.float64))
         assert rel_rms(y[c], ref) <= 1e-5
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", [(O.RR64, np.float64, np.float64), (O.RC64, np.float64, np.complex128)])
+def test_active_lag_scan_request_stays_reference_exact(dt, cdt, sdt):
+    """active_lag (poles at z = 1 and 1 - 1.6e-6, the reference demo src/main.rs:37-40) integrates
+    its input: carried through powers of A its states lose 3-6 digits against the reference-order
+    loop (host probe in runtime_iir.cpp), so even with the scan requested the handle runs the
+    serial recurrence -- bit-identical to the reference."""
+    num, den = O.active_lag(*ACTIVE_LAG)
+    rng = np.random.default_rng(dt)
+    x = rand(rng, 100000, sdt)
+    f = IIRFilter(num, den, SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    assert f.wscan_mode() == 0
+    y = np.concatenate([f.execute_block(x[:30000]), f.execute_block(x[30000:])])
+    assert bits_equal(y, O.iir(dt, num, den, O.SECOND_ORDER).execute_block(x))
+
+
+@pytest.mark.parametrize("dt,cdt,sdt,tol", [(O.RR64, np.float64, np.float64, 1e-12),
+                                            (O.RC64, np.float64, np.complex128, 1e-12),
+                                            (O.RR32, np.float32, np.float32, 2e-5),
+                                            (O.RC32, np.float32, np.complex64, 2e-5)])
+@pytest.mark.parametrize("kind", ["integrator", "resonator"])
+def test_exact_carry_scan_nondecaying(dt, cdt, sdt, tol, kind):
+    """cascades whose state response never decays (a pole at z = 1; a pair on the unit circle)
+    but stays well conditioned: no warm-up applies, so the wave scan carries exactly between
+    waves (aggregate pass + carry scan + output pass), ragged calls and decimation included"""
+    w = 2 * np.pi * 0.01
+    if kind == "integrator":  # y = sum x, cascaded with a decaying lowpass section
+        ff = np.array([1.0, 0.0, 0.0, 0.2, 0.2, 0.0])
+        fb = np.array([1.0, -1.0, 0.0, 1.0, -0.6, 0.0])
+    else:  # undamped resonator at f = 0.01
+        ff = np.array([1.0, 0.0, 0.0])
+        fb = np.array([1.0, -2.0 * np.cos(w), 1.0])
+    ff, fb = ff.astype(cdt), fb.astype(cdt)
+    rng = np.random.default_rng(dt + len(kind))
+    n = (1 << 19) + 777
+    x = rand(rng, n, sdt)
+    f = IIRFilter(ff, fb, SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    assert f.wscan_mode() == 2
+    cuts = [0, 9000, 9001, 300000, n]
+    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(cuts, cuts[1:])])
+    ref_dt = O.RC64 if np.dtype(sdt).kind == "c" else O.RR64
+    xr = x.astype(np.complex128 if np.dtype(sdt).kind == "c" else np.float64)
+    ref = O.iir(ref_dt, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER).execute_block(xr)
+    if cdt == np.float32:  # f32: as accurate as the reference-order f32 loop, both against f64
+        tol = max(tol, 10 * rel_rms(O.iir(dt, ff, fb, O.SECOND_ORDER).execute_block(x), ref))
+    assert rel_rms(y, ref) <= tol, (rel_rms(y, ref), tol)
+    g = DecimatingIIRFilter(ff, fb, SO, 3, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    yd = np.concatenate([g.execute_block(x[a:b]) for a, b in zip(cuts, cuts[1:])])
+    refd = O.iir_decim(ref_dt, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER, 3).execute_block(xr)
+    assert len(yd) == len(refd) and rel_rms(yd, refd) <= tol
