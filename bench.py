@@ -19,6 +19,7 @@ SURVEY §8f rows (build-defined cases, same parity + measurement fields):
   9  AGC bank, Complex<f64>, 2^18 channels x 2^10 samples
  10  32x interpolating FIR (K = 8), crcf, 2^25 inputs -> 2^30 outputs
  11  IIRFilter<f64, Complex<f64>> active_lag bank (the reference demo's filter), 2^16 channels x 2^12
+ 12  Normal DF-II IIR, order 2, real f32, 2^30 samples (dense-system wave scan)
 
 With N ranks each rank processes its own independent channel(s) (weak
 scaling, no collective in the timed region); RCCL is used afterwards only for
@@ -51,7 +52,7 @@ def parse():
                    help="ranks (one per GPU); outside torch.distributed.run this process spawns them itself")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", type=int, default=2, choices=list(range(1, 12)))
+    p.add_argument("--config", type=int, default=2, choices=list(range(1, 13)))
     p.add_argument("--log2n", type=int, default=30, help="samples per GPU per step (configs 2-4)")
     p.add_argument("--algo", default="fft", choices=["fft", "exact", "fma"], help="config 2 kernel")
     p.add_argument("--cpu-samples", type=int, default=None,
@@ -825,11 +826,59 @@ class Cfg11ActiveLag:
                          "(active_lag, one channel)", samples, CPU_CHUNK)
 
 
+class Cfg12Normal:
+    """IIRFilter<f32, f32> Normal DF-II (src/filter/iir/mod.rs:272-279) on the first biquad of the
+    cfg3 cascade as one polynomial pair, real f32, 2^30 samples: the dense-system wave scan."""
+    metric = "Msamples/sec Normal DF-II IIR (order 2, f32, 1 GiS); % HBM roofline"
+    tol = 1e-5
+
+    def __init__(self, args, rank, dev, torch, sd):
+        from solid_dsp_amd import IIRFilter, IIRFilterType
+        sos = np.array(json.load(open(os.path.join(REPO, "tests", "golden", "butter8_0p2_sos.json")))["sos"])
+        self.b, self.a = sos[0, :3].astype(np.float32), sos[0, 3:].astype(np.float32)
+        self.n = 1 << args.log2n
+        self.make = lambda d=dev: IIRFilter(self.b, self.a, IIRFilterType.Normal, sample_dtype=np.float32, device=d,
+                                            algo=sd.ALGO_FMA)
+        self.f = self.make()
+        self.d_in = torch.empty(self.n, dtype=torch.float32, device="cuda")
+        self.d_out = torch.empty(self.n, dtype=torch.float32, device="cuda")
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, self.n,
+                                       torch.cuda.current_stream().cuda_stream)
+        self.samples_per_step = self.n
+        self.bytes_per_step = 8 * self.n
+        self.dtype = "f32 (f32 coefficients, real f32 samples)"
+        self.kernel = "sos_wscan_kernel<0, 2, float, float> (dense 2-state system, 256-byte chunks)"
+        self.workload = f"cfg12: Normal DF-II order 2 (cfg3's first biquad), real f32, 2^{args.log2n} samples"
+        self.algo_name = "normal_scan"
+
+    def step(self, stream):
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+    def parity(self, stream, rng):
+        import oracle_lib as O
+        import torch
+        m = 1 << 20
+        g = self.make()
+        g.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        torch.cuda.synchronize()
+        x = self.d_in[:m].cpu().numpy().astype(np.float64)
+        y = self.d_out[:m].cpu().numpy()
+        ref = O.iir(O.RR64, self.b.astype(np.float64), self.a.astype(np.float64), O.NORMAL).execute_block(x)
+        return float(np.linalg.norm(y - ref) / np.linalg.norm(ref))
+
+    def cpu(self, samples):
+        import oracle_lib as O
+        x = O.synth(SEED, 0, 0, CPU_CHUNK).astype(np.float64)
+        f = O.iir(O.RR64, self.b.astype(np.float64), self.a.astype(np.float64), O.NORMAL)
+        return timed_cpu(lambda c: f.execute_block(x), "IIRFilter<f64, f64> Normal restatement (Window + two "
+                         "DotProducts per sample)", samples, CPU_CHUNK)
+
+
 WORKLOADS = {1: Cfg1FIR, 2: Cfg2FIR, 3: Cfg3IIR, 4: Cfg4Decim, 5: Cfg5Chan, 6: Cfg6ACorr, 7: Cfg7NCO, 8: Cfg8FFT, 9: Cfg9AGC,
-             10: Cfg10Interp, 11: Cfg11ActiveLag}
+             10: Cfg10Interp, 11: Cfg11ActiveLag, 12: Cfg12Normal}
 # bounded CPU samples: about 10-20 s of single-thread work each on a current x86 host
 CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 << 25, 7: 1 << 28, 8: 1 << 24, 9: 1 << 25,
-               10: 1 << 30, 11: 1 << 28}
+               10: 1 << 30, 11: 1 << 26, 12: 1 << 27}
 CPU_CHUNK = 1 << 22
 
 

@@ -92,6 +92,55 @@ __device__ __forceinline__ void matvec_lt(const C* __restrict__ P, const I (&x)[
     }
 }
 
+template <int D, typename C, typename I>
+__device__ __forceinline__ void matvec_full(const C* __restrict__ P, const I (&x)[D], I (&y)[D]) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        I acc = mul_(P[r * D], x[0]);
+#pragma unroll
+        for (int c = 1; c < D; ++c) acc = fmac_(acc, P[r * D + c], x[c]);
+        y[r] = acc;
+    }
+}
+
+// one step of the scanned system.  ND == 0: the SOS cascade, state (w1_q, w2_q) at
+// st[2q], st[2q+1] (the fused form of sos_step_f).  ND > 0: Normal DF-II
+// (src/filter/iir/mod.rs:272-279) with ND states hh[i] = v[n-1-i]; coefficients
+// num[0..ND] then den[0..ND) (a[1..] / a0), zero padded to those lengths:
+//   v = x - den . hh,   y = num[0] v + num[1..] . hh,   hh <- (v, hh[0..ND-2])
+template <int S, int ND, typename C, typename I>
+__device__ __forceinline__ I sys_step(const C* __restrict__ c, I v, I (&st)[ND ? ND : 2 * S]) {
+    if constexpr (ND == 0) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            const I w = fmac_(fmac_(v, -c[5 * q + 4], st[2 * q + 1]), -c[5 * q + 3], st[2 * q]);
+            v = fmac_(fmac_(mul_(c[5 * q + 2], st[2 * q + 1]), c[5 * q + 1], st[2 * q]), c[5 * q + 0], w);
+            st[2 * q + 1] = st[2 * q];
+            st[2 * q] = w;
+        }
+        return v;
+    } else {
+        I d = mul_(c[ND + 1], st[0]);
+#pragma unroll
+        for (int i = 1; i < ND; ++i) d = fmac_(d, c[ND + 1 + i], st[i]);
+        const I w = sub_(v, d);
+        I out = mul_(c[0], w);
+#pragma unroll
+        for (int i = 1; i <= ND; ++i) out = fmac_(out, c[i], st[i - 1]);
+#pragma unroll
+        for (int i = ND - 1; i > 0; --i) st[i] = st[i - 1];
+        st[0] = w;
+        return out;
+    }
+}
+
+// y = P x: lower block-triangular for SOS cascades, dense for Normal DF-II
+template <int ND, int D, typename C, typename I>
+__device__ __forceinline__ void sys_matvec(const C* __restrict__ P, const I (&x)[D], I (&y)[D]) {
+    if constexpr (ND == 0) matvec_lt<D>(P, x, y);
+    else matvec_full<D>(P, x, y);
+}
+
 using v4u = unsigned __attribute__((ext_vector_type(4)));
 
 template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / sizeof(I)]) {
@@ -105,14 +154,14 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // Mi > 1 the staged domain sample k is x[k / Mi] at k % Mi == 0, else zero; with
 // Md > 1 only domain samples k = j0 + o Md are stored, as y[o] (gathered from the
 // slab so that 64 consecutive outputs leave per store instruction).
-template <int S, typename C, typename I, int CB, bool RERUN>
+template <int S, int ND, typename C, typename I, int CB, bool RERUN>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
                  const I* __restrict__ st_in, I* __restrict__ st_out, long long nd, int wc, int tpw, bool vec_ok,
                  int Mi, int Md, long long j0, long long nout, const I* __restrict__ cin, I* __restrict__ gagg,
                  long long nwaves) {
-    constexpr int D = 2 * S;
+    constexpr int D = ND ? ND : 2 * S;
     constexpr int B = ws_chunk<I, CB>::B;
     constexpr int E = 16 / (int)sizeof(I);  // samples per 16-byte vector
     constexpr int kRowBytes = WsGeom<CB>::kRowBytes, kVecPerRow = WsGeom<CB>::kVecPerRow;
@@ -201,20 +250,17 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         // 2. zero-state run over my row, y0 in place
         I s[D];
         {
-            I w1[S], w2[S];
 #pragma unroll
-            for (int q = 0; q < S; ++q) { w1[q] = zero_v<I>(); w2[q] = zero_v<I>(); }
+            for (int d = 0; d < D; ++d) s[d] = zero_v<I>();
 #pragma unroll 2
             for (int o = 0; o < kVecPerRow; ++o) {
                 I e[E];
                 const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
                 __builtin_memcpy(e, &val, 16);
 #pragma unroll
-                for (int i = 0; i < E; ++i) e[i] = sos_step_f<S>(coefs, e[i], w1, w2);
+                for (int i = 0; i < E; ++i) e[i] = sys_step<S, ND>(coefs, e[i], s);
                 if constexpr (!RERUN) *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
             }
-#pragma unroll
-            for (int q = 0; q < S; ++q) { s[2 * q] = w1[q]; s[2 * q + 1] = w2[q]; }
         }
         if (!cin && !agg && gw == 0 && t == 0 && lane == wc - 1) {  // the call's exact carried state enters here
 #pragma unroll
@@ -223,7 +269,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         // 3. fold the carry into lane 0, then the inclusive scan over lanes
         {
             I a[D];
-            matvec_lt<D>(sP, carry, a);
+            sys_matvec<ND>(sP, carry, a);
             if (lane == 0) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) s[d] = add_(s[d], a[d]);
@@ -235,7 +281,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             I prev[D], a[D];
 #pragma unroll
             for (int d = 0; d < D; ++d) prev[d] = shfl_up_v(s[d], off);
-            matvec_lt<D>(sP + k * D * D, prev, a);
+            sys_matvec<ND>(sP + k * D * D, prev, a);
             if (lane >= off) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) s[d] = add_(s[d], a[d]);
@@ -257,16 +303,16 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         // 4. outputs: correction by the state response (y0 in place), or (RERUN) the
         //    chunk rerun from its true initial state over the staged input
         if constexpr (RERUN) {
-            I w1[S], w2[S];
+            I st[D];
 #pragma unroll
-            for (int q = 0; q < S; ++q) { w1[q] = init[2 * q]; w2[q] = init[2 * q + 1]; }
+            for (int d = 0; d < D; ++d) st[d] = init[d];
 #pragma unroll 2
             for (int o = 0; o < kVecPerRow; ++o) {
                 I e[E];
                 const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
                 __builtin_memcpy(e, &val, 16);
 #pragma unroll
-                for (int i = 0; i < E; ++i) e[i] = sos_step_f<S>(coefs, e[i], w1, w2);
+                for (int i = 0; i < E; ++i) e[i] = sys_step<S, ND>(coefs, e[i], st);
                 *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
             }
         } else {
@@ -288,12 +334,12 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         // exact final state: the lane of this segment holding sample nd-1 reruns its chunk
         const long long kc = k0 + (long long)lane * B;
         if (kc >= k_lo && kc <= nd - 1 && nd - 1 < kc + B) {
-            I w1[S], w2[S];
+            I st[D];
 #pragma unroll
-            for (int q = 0; q < S; ++q) { w1[q] = init[2 * q]; w2[q] = init[2 * q + 1]; }
-            for (long long k = kc; k < nd; ++k) (void)sos_step_f<S>(coefs, dom(k), w1, w2);
+            for (int d = 0; d < D; ++d) st[d] = init[d];
+            for (long long k = kc; k < nd; ++k) (void)sys_step<S, ND>(coefs, dom(k), st);
 #pragma unroll
-            for (int q = 0; q < S; ++q) { st_out[2 * q] = w1[q]; st_out[2 * q + 1] = w2[q]; }
+            for (int d = 0; d < D; ++d) st_out[d] = st[d];
         }
         wave_sync();
 
@@ -342,16 +388,6 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 // cin[0] = st_in, cin[w + 1] = Phi cin[w] + G[w].  Each of the 256 lanes folds a
 // contiguous run of R waves (Horner with Phi), lane 0 chains the 256 run
 // aggregates with Phi^R, then every lane replays its run from its exact prefix.
-template <int D, typename C, typename I>
-__device__ __forceinline__ void matvec_full(const C* __restrict__ P, const I (&x)[D], I (&y)[D]) {
-#pragma unroll
-    for (int r = 0; r < D; ++r) {
-        I acc = mul_(P[r * D], x[0]);
-#pragma unroll
-        for (int c = 1; c < D; ++c) acc = fmac_(acc, P[r * D + c], x[c]);
-        y[r] = acc;
-    }
-}
 
 template <int D, typename C, typename I>
 __global__ void __launch_bounds__(256)
@@ -732,10 +768,10 @@ template <int CB> int wscan_tpw(long long nch) {
     return tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
 }
 
-template <typename C, typename I, int S, int CB, bool RERUN>
+template <typename C, typename I, int S, int CB, bool RERUN, int ND = 0>
 hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     constexpr int B = ws_chunk<I, CB>::B;
-    constexpr int D = 2 * S;
+    constexpr int D = ND ? ND : 2 * S;
     const long long nd = (long long)a.n * a.Mi;  // domain samples
     const long long nch = (nd + B - 1) / B;
     const int tpw = wscan_tpw<CB>(nch);
@@ -747,18 +783,18 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     // 16-byte vector path: aligned bases and channel strides
     const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
                         (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
-    const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * 4 * S * S + B * 2 * S);
+    const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * D * D + B * D);
     const long long j0 = a.Md > 1 ? (long long)((a.Md - 1 - a.phase) % a.Md) : 0;  // first emitting domain index
     const long long ny = a.Md > 1 ? (long long)a.nout : nd;
     if (exact) {
-        hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
+        hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
                            (I*)a.y, (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out,
                            nd, 0, tpw, vec_ok, a.Mi, a.Md, j0, ny, (const I*)nullptr, (I*)a.G, waves);
         hipLaunchKernelGGL((wscan_carry_kernel<D, C, I>), dim3((unsigned)a.channels), dim3(256), 0, st,
                            (const I*)a.G, (I*)a.Cin, (const C*)a.Phi + (size_t)(tpw - 1) * D * D, (const I*)a.st_in,
                            waves);
     }
-    hipLaunchKernelGGL((sos_wscan_kernel<S, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
+    hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
                        tpw, vec_ok, a.Mi, a.Md, j0, ny, exact ? (const I*)a.Cin : (const I*)nullptr, (I*)nullptr,
                        waves);
@@ -780,8 +816,25 @@ hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+// Normal DF-II with D = cap - 1 states (D <= 8), 256-byte chunks
+template <typename C, typename I>
+hipError_t launch_wscan_normal(const IirArgs& a, hipStream_t st) {
+    switch (a.cap - 1) {
+        case 1: return launch_wscan_t<C, I, 0, 256, false, 1>(a, st);
+        case 2: return launch_wscan_t<C, I, 0, 256, false, 2>(a, st);
+        case 3: return launch_wscan_t<C, I, 0, 256, false, 3>(a, st);
+        case 4: return launch_wscan_t<C, I, 0, 256, false, 4>(a, st);
+        case 5: return launch_wscan_t<C, I, 0, 256, false, 5>(a, st);
+        case 6: return launch_wscan_t<C, I, 0, 256, false, 6>(a, st);
+        case 7: return launch_wscan_t<C, I, 0, 256, false, 7>(a, st);
+        case 8: return launch_wscan_t<C, I, 0, 256, false, 8>(a, st);
+    }
+    return hipErrorInvalidValue;
+}
+
 template <typename C, typename I>
 hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
+    if (a.sections == 0) return launch_wscan_normal<C, I>(a, st);
     if (a.Mi != 1 || a.Md != 1 || a.wc == 0)  // rate changes / exact carries: the single-chunk kernels only
         return a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st) : launch_wscan_s<C, I, 256>(a, st);
     if constexpr (std::is_same<I, float>::value) {

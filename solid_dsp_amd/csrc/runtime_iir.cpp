@@ -100,7 +100,7 @@ struct sdsp_iir {
     std::vector<unsigned char> cdev;     // normalised coefficients in the Coef type (device layout)
     int S = 0, nb = 0, na = 0, cap = 0;
     std::vector<Group> groups;
-    DevBuf d_coefs, d_state[2], d_tmp[2], d_carry[2];
+    DevBuf d_coefs, d_coefs_nrm, d_state[2], d_tmp[2], d_carry[2];
     int cur = 0;
     int algo = SDSP_ALGO_EXACT;  // reference-order recurrence unless the caller opts in (sdsp.h)
     int wscan = 1;  // 0: block scan; 1-4: wave-scan variant 0-3 (kern_iir_wscan.hip; sdsp_iir_set_tuning)
@@ -140,38 +140,39 @@ int iir_alloc_state(sdsp_iir* h) {
     return SDSP_OK;
 }
 
-// state-transition matrix of sections [first, first+count) with x = 0
-Mat sos_A(const sdsp_iir* h, int first, int count) {
-    const int D = 2 * count;
-    Mat A(D * D, 0.0);
-    for (int j = 0; j < D; ++j) {
-        std::vector<double> w1(count), w2(count);
-        for (int q = 0; q < count; ++q) { w1[q] = (2 * q == j) ? 1.0 : 0.0; w2[q] = (2 * q + 1 == j) ? 1.0 : 0.0; }
-        double v = 0.0;
-        for (int q = 0; q < count; ++q) {
-            const double* c = &h->c64[5 * (first + q)];
-            const double d = c[3] * w1[q] + c[4] * w2[q];
-            const double w = v - d;
-            v = c[0] * w + c[1] * w1[q] + c[2] * w2[q];
-            w2[q] = w1[q];
-            w1[q] = w;
-        }
-        for (int q = 0; q < count; ++q) {
-            A[(2 * q) * D + j] = w1[q];
-            A[(2 * q + 1) * D + j] = w2[q];
-        }
-    }
-    return A;
-}
 
-// run sections [first, first+count) over x from state s (in place), f64
-void sos_run(const sdsp_iir* h, const Group& g, const double* x, double* y, size_t n, std::vector<double>& s) {
+// state dimension of a scanned group: the SOS sections' (w1, w2) pairs, or the
+// Normal DF-II delay line (cap - 1 values)
+int group_dim(const sdsp_iir* h, const Group& g) { return h->type == 1 ? 2 * g.count : h->cap - 1; }
+
+// run the group's system over x from state s (in place) in precision T: sections
+// [first, first+count) of the SOS cascade (sos.rs:92-114), or the Normal DF-II
+// recurrence (mod.rs:272-279).  The coefficients are the handle's (already rounded
+// to the Coef type), so T = float reproduces an f32 handle's arithmetic.
+template <typename T>
+void sys_run(const sdsp_iir* h, const Group& g, const T* x, T* y, size_t n, std::vector<T>& s) {
+    if (h->type == 0) {
+        const int D = h->cap - 1, nb = h->nb, na1 = h->na - 1;
+        const double* num = h->c64.data();
+        const double* den = h->c64.data() + nb;
+        for (size_t k = 0; k < n; ++k) {
+            T d = 0;
+            for (int i = 0; i < na1; ++i) d += (T)den[i] * s[i];
+            const T v = x[k] - d;
+            T out = (T)num[0] * v;
+            for (int i = 1; i < nb; ++i) out += (T)num[i] * s[i - 1];
+            for (int i = D - 1; i > 0; --i) s[i] = s[i - 1];
+            if (D > 0) s[0] = v;
+            if (y) y[k] = out;
+        }
+        return;
+    }
     for (size_t i = 0; i < n; ++i) {
-        double v = x[i];
+        T v = x[i];
         for (int q = 0; q < g.count; ++q) {
             const double* c = &h->c64[5 * (g.first + q)];
-            const double w = v - (c[3] * s[2 * q] + c[4] * s[2 * q + 1]);
-            v = c[0] * w + c[1] * s[2 * q] + c[2] * s[2 * q + 1];
+            const T w = v - ((T)c[3] * s[2 * q] + (T)c[4] * s[2 * q + 1]);
+            v = (T)c[0] * w + (T)c[1] * s[2 * q] + (T)c[2] * s[2 * q + 1];
             s[2 * q + 1] = s[2 * q];
             s[2 * q] = w;
         }
@@ -179,47 +180,82 @@ void sos_run(const sdsp_iir* h, const Group& g, const double* x, double* y, size
     }
 }
 
+// state-transition matrix of the group's system (zero input), row-major
+Mat sys_A(const sdsp_iir* h, const Group& g) {
+    const int D = group_dim(h, g);
+    Mat A(D * D, 0.0);
+    const double zero = 0.0;
+    for (int j = 0; j < D; ++j) {
+        std::vector<double> s(D, 0.0);
+        s[j] = 1.0;
+        sys_run<double>(h, g, &zero, nullptr, 1, s);
+        for (int i = 0; i < D; ++i) A[i * D + j] = s[i];
+    }
+    return A;
+}
+
 // Is carrying chunk states through A^B as accurate as the recurrence itself?  A
 // cascade that integrates its input (e.g. active_lag: poles at 1 and 1 - 1.6e-6)
-// grows states ~1e6 x its output, and re-associating the recurrence through
-// powers of A then loses 3-6 digits against the reference-order loop (measured:
-// 8e-6 relative at 2^18 samples, against 2e-9 for the serial f64 loop).  A host
-// probe in f64 -- zero-state chunks corrected by exactly carried states, against
-// the serial loop over 2^14 pseudo-random samples -- admits the exact-carry scan
-// only when the two agree to 1e-11.
-bool carry_well_conditioned(const sdsp_iir* h, const Group& g, int B, const Mat& AB) {
-    const int D = 2 * g.count;
-    const size_t n = 1 << 14;
-    std::vector<double> x(n), ys(n), yc(n);
-    uint64_t r = 0x9E3779B97F4A7C15ULL;
-    for (auto& v : x) {
-        r = r * 6364136223846793005ULL + 1442695040888963407ULL;
-        v = (double)(r >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+// grows states ~1e6 x its output, and re-associating the recurrence through powers
+// of A then loses 3-6 digits against the reference-order loop (measured: 8e-6
+// relative at 2^18 samples, against 2e-9 for the serial f64 loop); a high-order
+// direct-form polynomial does the same through its companion matrix.  Host probe
+// over 2^14 pseudo-random samples in the handle's precision T: zero-state chunks
+// corrected by carried states against the serial loop, both measured against the
+// serial loop in f64; admitted when the carried form is within 10x the serial
+// form's own error (plus 1e-13 / 1e-7 of slack).
+template <typename T>
+double probe_rel(const std::vector<T>& a, const std::vector<double>& ref) {
+    double num = 0.0, den = 0.0;
+    for (size_t i = 0; i < ref.size(); ++i) {
+        num += ((double)a[i] - ref[i]) * ((double)a[i] - ref[i]);
+        den += ref[i] * ref[i];
     }
-    std::vector<double> st(D, 0.0);
-    sos_run(h, g, x.data(), ys.data(), n, st);
-    std::vector<double> I(D, 0.0), e(D), cr(D * (size_t)B);
+    return (std::isfinite(num) && den > 0.0) ? std::sqrt(num / den) : INFINITY;
+}
+
+template <typename T>
+bool carry_well_conditioned_t(const sdsp_iir* h, const Group& g, int B, const Mat& AB) {
+    const int D = group_dim(h, g);
+    const size_t n = 1 << 14;
+    std::vector<double> x64(n), ref(n);
+    uint64_t r = 0x9E3779B97F4A7C15ULL;
+    for (auto& v : x64) {
+        r = r * 6364136223846793005ULL + 1442695040888963407ULL;
+        v = (double)(float)((double)(r >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0);
+    }
+    std::vector<double> s64(D, 0.0);
+    sys_run<double>(h, g, x64.data(), ref.data(), n, s64);
+    std::vector<T> x(x64.begin(), x64.end()), ys(n), yc(n);
+    std::vector<T> st(D, 0);
+    sys_run<T>(h, g, x.data(), ys.data(), n, st);
+    std::vector<T> cr(D * (size_t)B), ABt(AB.begin(), AB.end());
     for (int d = 0; d < D; ++d) {  // Cr[i][d]: output response to basis state e_d
-        std::vector<double> zs(D, 0.0), zero(B, 0.0), out(B);
-        zs[d] = 1.0;
-        sos_run(h, g, zero.data(), out.data(), B, zs);
+        std::vector<T> zs(D, 0), zero(B, 0), out(B);
+        zs[d] = 1;
+        sys_run<T>(h, g, zero.data(), out.data(), B, zs);
         for (int i = 0; i < B; ++i) cr[(size_t)i * D + d] = out[i];
     }
+    std::vector<T> I(D, 0), e(D), nI(D);
     for (size_t k = 0; k < n; k += B) {
-        std::fill(e.begin(), e.end(), 0.0);
-        sos_run(h, g, &x[k], &yc[k], B, e);
+        std::fill(e.begin(), e.end(), T(0));
+        sys_run<T>(h, g, &x[k], &yc[k], B, e);
         for (int i = 0; i < B; ++i)
             for (int d = 0; d < D; ++d) yc[k + i] += cr[(size_t)i * D + d] * I[d];
-        std::vector<double> nI(D, 0.0);
         for (int a = 0; a < D; ++a) {
-            for (int b = 0; b < D; ++b) nI[a] += AB[a * D + b] * I[b];
-            nI[a] += e[a];
+            T v = 0;
+            for (int b = 0; b < D; ++b) v += ABt[a * D + b] * I[b];
+            nI[a] = v + e[a];
         }
         I = nI;
     }
-    double num = 0.0, den = 0.0;
-    for (size_t i = 0; i < n; ++i) { num += (yc[i] - ys[i]) * (yc[i] - ys[i]); den += ys[i] * ys[i]; }
-    return std::isfinite(num) && den > 0.0 && std::sqrt(num / den) <= 1e-11;
+    const double e_ser = probe_rel(ys, ref), e_car = probe_rel(yc, ref);
+    return e_car <= 10.0 * e_ser + (sizeof(T) == 8 ? 1e-13 : 1e-7);
+}
+
+bool carry_well_conditioned(const sdsp_iir* h, const Group& g, int B, const Mat& AB) {
+    return is_f32(h->dtype) ? carry_well_conditioned_t<float>(h, g, B, AB)
+                            : carry_well_conditioned_t<double>(h, g, B, AB);
 }
 
 // Scan tables for chunks of B samples: warm-up chunks wc (smallest m with
@@ -229,8 +265,8 @@ bool carry_well_conditioned(const sdsp_iir* h, const Group& g, int B, const Mat&
 int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, int* wc, DevBuf* dP, DevBuf* dCr,
                 DevBuf* dPhi = nullptr, bool* exact = nullptr) {
     const double tol = is_f32(h->dtype) ? 1e-9 : 1e-17;
-    const int D = 2 * g.count;
-    const Mat A = sos_A(h, g.first, g.count);
+    const int D = group_dim(h, g);
+    const Mat A = sys_A(h, g);
     const Mat AB = matpow(A, B, D);
     Mat Am = AB;
     *wc = 0;
@@ -241,6 +277,10 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
         Am = matmul(Am, AB, D);
     }
     if (exact) *exact = false;
+    if (*wc > 0 && h->type == 0 && !carry_well_conditioned(h, g, B, AB)) {
+        *wc = 0;  // a direct-form polynomial whose companion powers lose digits: serial only
+        return SDSP_OK;
+    }
     if (*wc == 0) {
         // a state response that does not die out (e.g. a pole at z = 1, the active_lag PLL
         // filter): exact carries between waves instead of warm-up, provided the powers of A
@@ -270,20 +310,11 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
     IIR_TRY(hipMemcpy(dP->p, P.data(), P.size(), hipMemcpyHostToDevice), "copy P");
     if (!dCr) return SDSP_OK;
     std::vector<double> resp((size_t)B * D);
-    for (int d = 0; d < D; ++d) {
-        std::vector<double> w1(g.count), w2(g.count);
-        for (int q = 0; q < g.count; ++q) { w1[q] = (2 * q == d) ? 1.0 : 0.0; w2[q] = (2 * q + 1 == d) ? 1.0 : 0.0; }
-        for (int i = 0; i < B; ++i) {
-            double v = 0.0;
-            for (int q = 0; q < g.count; ++q) {
-                const double* c = &h->c64[5 * (g.first + q)];
-                const double w = v - (c[3] * w1[q] + c[4] * w2[q]);
-                v = c[0] * w + c[1] * w1[q] + c[2] * w2[q];
-                w2[q] = w1[q];
-                w1[q] = w;
-            }
-            resp[(size_t)i * D + d] = v;
-        }
+    for (int d = 0; d < D; ++d) {  // output response to basis state e_d, zero input
+        std::vector<double> st(D, 0.0), zero(B, 0.0), out(B);
+        st[d] = 1.0;
+        sys_run<double>(h, g, zero.data(), out.data(), B, st);
+        for (int i = 0; i < B; ++i) resp[(size_t)i * D + d] = out[i];
     }
     std::vector<unsigned char> Cr;
     for (double v : resp) push_coef(Cr, v, h->dtype);
@@ -294,6 +325,23 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
 
 int plan_groups(sdsp_iir* h) {
     h->groups.clear();
+    if (h->type == 0) {  // Normal DF-II: one dense system of cap - 1 states on the wave scan (D <= 8)
+        const int D = h->cap - 1;
+        if (D < 1 || D > 8) return SDSP_OK;
+        h->groups.emplace_back();
+        Group& g = h->groups.back();
+        const int Bw = iir_wscan_chunk(h->dtype, 0);
+        int st = scan_tables(h, g, Bw, 32, 7, &g.ws[0].wc, &g.ws[0].d_P, &g.ws[0].d_Cr, &g.ws[0].d_Phi,
+                             &g.ws[0].exact);
+        if (st) return st;
+        // the kernel's coefficient layout: num[0..D] then den[0..D), zero padded
+        std::vector<unsigned char> c;
+        for (int i = 0; i <= D; ++i) push_coef(c, i < h->nb ? h->c64[i] : 0.0, h->dtype);
+        for (int i = 0; i < D; ++i) push_coef(c, i < h->na - 1 ? h->c64[h->nb + i] : 0.0, h->dtype);
+        IIR_TRY(h->d_coefs_nrm.ensure(c.size()), "alloc normal coefs");
+        IIR_TRY(hipMemcpy(h->d_coefs_nrm.p, c.data(), c.size(), hipMemcpyHostToDevice), "copy normal coefs");
+        return SDSP_OK;
+    }
     if (h->type != 1) return SDSP_OK;
     for (int f = 0; f < h->S; f += kMaxGroupSections) {
         h->groups.emplace_back();
@@ -416,6 +464,7 @@ int iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void
 
 // wave-scan variant index for this group (-1: none applies)
 int group_wscan(const sdsp_iir* h, const Group& g, bool rate_change) {
+    if (h->type == 0) return (h->wscan >= 1 && (g.ws[0].wc > 0 || g.ws[0].exact)) ? 0 : -1;
     int wv = h->wscan - 1;
     if ((rate_change || g.wc == 0) && (wv == 2 || wv == 3)) wv = 0;  // paired kernels: decaying, no rate change
     if (wv < 0) return -1;
@@ -423,7 +472,7 @@ int group_wscan(const sdsp_iir* h, const Group& g, bool rate_change) {
 }
 
 bool group_scan(const sdsp_iir* h, const Group& g, size_t nd, bool rate_change) {
-    if (h->type != 1) return false;
+    if (h->type == 0 && group_wscan(h, g, rate_change) < 0) return false;
     if (g.wc == 0 && group_wscan(h, g, rate_change) < 0) return false;
     if (h->algo == SDSP_ALGO_EXACT) return false;
     if (h->algo == SDSP_ALGO_AUTO && nd < 8192) return false;
@@ -468,6 +517,7 @@ void sdsp_iir_destroy(sdsp_iir* h) {
             (void)hipStreamDestroy(h->stream);
         }
         h->d_coefs.release();
+        h->d_coefs_nrm.release();
         for (int i = 0; i < 2; ++i) { h->d_state[i].release(); h->d_tmp[i].release(); h->d_carry[i].release(); }
         for (auto& g : h->groups) {
             g.d_P.release();
@@ -563,7 +613,29 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
     if (h->type == 0) {
         IirArgs a{d_in, d_out, h->d_coefs.p, nullptr, st_in, st_out, n, nout, h->channels, 0, h->nb, h->na, h->cap,
                   Mi, Md, h->phase, false, 0};
-        IIR_TRY(launch_iir(h->dtype, a, s), "iir normal");
+        const bool rc = Mi != 1 || Md != 1;
+        if (!h->groups.empty() && group_scan(h, h->groups[0], nd, rc)) {  // dense-system wave scan
+            const Group& gr = h->groups[0];
+            a.coefs = h->d_coefs_nrm.p;
+            a.algo_scan = true;
+            a.P = gr.ws[0].d_P.p;
+            a.Cr = gr.ws[0].d_Cr.p;
+            a.wc = gr.ws[0].wc;
+            a.ws_variant = 0;
+            if (a.wc == 0) {
+                a.Phi = gr.ws[0].d_Phi.p;
+                const size_t W = iir_wscan_waves(h->dtype, a);
+                const size_t bytes = h->channels * W * (size_t)(h->cap - 1) * sbytes;
+                IIR_TRY(h->d_carry[0].ensure(bytes), "iir carry scratch");
+                IIR_TRY(h->d_carry[1].ensure(bytes), "iir carry scratch");
+                a.G = h->d_carry[0].p;
+                a.Cin = h->d_carry[1].p;
+                a.scratch_waves = W;
+            }
+            IIR_TRY(launch_iir_wscan(h->dtype, a, s), "iir normal wave scan");
+        } else {
+            IIR_TRY(launch_iir(h->dtype, a, s), "iir normal");
+        }
     } else {
         const size_t ng = h->groups.size();
         if (ng > 1) {

@@ -358,7 +358,9 @@ def test_exact_carry_scan_nondecaying(dt, cdt, sdt, tol, kind):
     n = (1 << 19) + 777
     x = rand(rng, n, sdt)
     f = IIRFilter(ff, fb, SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
-    assert f.wscan_mode() == 2
+    # the integrator is admitted by the host conditioning probe; the undamped resonator's
+    # carried form may or may not be (then the serial loop runs): accuracy is checked either way
+    assert f.wscan_mode() == 2 or (kind == "resonator" and f.wscan_mode() == 0)
     cuts = [0, 9000, 9001, 300000, n]
     y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(cuts, cuts[1:])])
     ref_dt = O.RC64 if np.dtype(sdt).kind == "c" else O.RR64
@@ -371,3 +373,29 @@ def test_exact_carry_scan_nondecaying(dt, cdt, sdt, tol, kind):
     yd = np.concatenate([g.execute_block(x[a:b]) for a, b in zip(cuts, cuts[1:])])
     refd = O.iir_decim(ref_dt, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER, 3).execute_block(xr)
     assert len(yd) == len(refd) and rel_rms(yd, refd) <= tol
+
+
+@pytest.mark.parametrize("dt,cdt,sdt,tol", [(O.RR32, np.float32, np.float32, 1e-5), (O.RC32, np.float32, np.complex64, 1e-5),
+                                            (O.RR64, np.float64, np.float64, 1e-12), (O.RC64, np.float64, np.complex128, 1e-12)])
+@pytest.mark.parametrize("order", [2, 4, 8])
+def test_normal_df2_wave_scan(dt, cdt, sdt, tol, order):
+    """Normal DF-II (src/filter/iir/mod.rs:272-279) on the dense-system wave scan: butter(order)
+    as a single polynomial pair, ragged calls, state carried into the serial kernel and back"""
+    from scipy import signal
+    b, a = signal.butter(order, 0.15)
+    b, a = b.astype(cdt), a.astype(cdt)
+    rng = np.random.default_rng(order + dt)
+    n = 200001
+    x = rand(rng, n, sdt)
+    f = IIRFilter(b, a, NORMAL, sample_dtype=sdt, algo=sd.ALGO_AUTO)
+    # low orders run on the wave scan; higher-order polynomials whose companion powers lose
+    # digits are kept on the serial loop by the host probe (accuracy is checked either way)
+    assert f.wscan_mode() == 1 if order == 2 else f.wscan_mode() in (0, 1)
+    cuts = [0, 100, 9000, 120000, 120050, n]  # AUTO: blocks < 8192 take the serial kernel
+    y = np.concatenate([f.execute_block(x[p:q]) for p, q in zip(cuts, cuts[1:])])
+    ref_dt = O.RC64 if np.dtype(sdt).kind == "c" else O.RR64
+    xr = x.astype(np.complex128 if np.dtype(sdt).kind == "c" else np.float64)
+    ref = O.iir(ref_dt, b.astype(np.float64), a.astype(np.float64), O.NORMAL).execute_block(xr)
+    if cdt == np.float32:  # a direct-form polynomial in f32: as accurate as the f32 reference loop
+        tol = max(tol, 10 * rel_rms(O.iir(dt, b, a, O.NORMAL).execute_block(x), ref))
+    assert rel_rms(y, ref) <= tol, (rel_rms(y, ref), tol)
