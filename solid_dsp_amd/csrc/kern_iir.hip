@@ -99,6 +99,92 @@ sos_serial_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restric
     }
 }
 
+// ---------------------------------------------------------------- serial SOS, LDS-staged
+// The same recurrence (lane = channel, reference order, bit-identical) for banks of
+// >= 64 channels without rate change: a one-wave workgroup serves 64 channels and
+// moves them through LDS in tiles of 256 bytes per channel, so HBM sees coalesced
+// 256-byte runs instead of one element per lane 8n bytes apart (measured 2.4x the
+// algorithmic traffic on the active_lag bank), with the next tile's loads in flight
+// while the current one runs.
+template <int S, typename C, typename I>
+__global__ void __launch_bounds__(64)
+sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
+                      const I* __restrict__ st_in, I* __restrict__ st_out, long long n, int channels, bool vec_ok) {
+    using v4u = unsigned __attribute__((ext_vector_type(4)));
+    constexpr int kRun = 256, E = 16 / (int)sizeof(I), T = kRun / (int)sizeof(I), kRow = kRun + 16;
+    __shared__ __attribute__((aligned(16))) char lds[64 * kRow];
+    const int lane = threadIdx.x;
+    const long long c0 = (long long)blockIdx.x * 64;
+    const int nch = channels - c0 < 64 ? (int)(channels - c0) : 64;
+    const int ch = (int)c0 + lane;
+    I w1[S], w2[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        w1[s] = lane < nch ? st_in[(long long)ch * 2 * S + 2 * s] : zero_v<I>();
+        w2[s] = lane < nch ? st_in[(long long)ch * 2 * S + 2 * s + 1] : zero_v<I>();
+    }
+    // vector v of a tile: channel v >> 4, 16-byte part v & 15
+    auto vaddr = [&](long long k0, int v) -> long long { return (c0 + (v >> 4)) * n + k0 + (long long)(v & 15) * E; };
+    v4u pre[16];
+    auto load_tile = [&](long long k0) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int v = lane + 64 * j;
+            pre[j] = (v >> 4) < nch ? *reinterpret_cast<const v4u*>(x + vaddr(k0, v)) : v4u{0, 0, 0, 0};
+        }
+    };
+    const bool fast = vec_ok;
+    if (fast && n >= T) load_tile(0);
+    for (long long k0 = 0; k0 < n; k0 += T) {
+        const bool full = fast && k0 + T <= n;
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int v = lane + 64 * j;
+                *reinterpret_cast<v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16) = pre[j];
+            }
+            if (k0 + 2 * T <= n) load_tile(k0 + T);  // next tile in flight during this one
+        } else {
+            for (int i = lane; i < 64 * T; i += 64) {
+                const int cl = i / T, e = i % T;
+                *reinterpret_cast<I*>(lds + cl * kRow + e * (int)sizeof(I)) =
+                    (cl < nch && k0 + e < n) ? x[(c0 + cl) * n + k0 + e] : zero_v<I>();
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        const int cnt = n - k0 < T ? (int)(n - k0) : T;
+        I* row = reinterpret_cast<I*>(lds + lane * kRow);
+        for (int e = 0; e < cnt; ++e) row[e] = sos_step<true, S>(coefs, row[e], w1, w2);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int v = lane + 64 * j;
+                if ((v >> 4) < nch)
+                    *reinterpret_cast<v4u*>(y + vaddr(k0, v)) =
+                        *reinterpret_cast<const v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16);
+            }
+        } else {
+            for (int i = lane; i < 64 * T; i += 64) {
+                const int cl = i / T, e = i % T;
+                if (cl < nch && k0 + e < n)
+                    y[(c0 + cl) * n + k0 + e] = *reinterpret_cast<const I*>(lds + cl * kRow + e * (int)sizeof(I));
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < nch) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            st_out[(long long)ch * 2 * S + 2 * s] = w1[s];
+            st_out[(long long)ch * 2 * S + 2 * s + 1] = w2[s];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- serial Normal DF-II
 // hh[i] = w[n-1-i] for i < cap-1 (newest first; the window's oldest slot is
 // never read by either dot product, src/filter/iir/mod.rs:272-279).
@@ -267,6 +353,13 @@ hipError_t launch_sos_t(const IirArgs& a, hipStream_t st) {
         hipLaunchKernelGGL((sos_scan_kernel<S, C, I>), grid, dim3(kScanT), lds, st, (const I*)a.x, (I*)a.y,
                            (const C*)a.coefs, (const C*)a.P, (const I*)a.st_in, (I*)a.st_out, (long long)a.n,
                            (long long)a.nout, a.Mi, a.Md, (long long)a.phase, a.wc);
+    } else if (a.Mi == 1 && a.Md == 1 && a.channels >= 64) {
+        dim3 grid((unsigned)((a.channels + 63) / 64));
+        const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
+                            (a.n * sizeof(I)) % 16 == 0;
+        hipLaunchKernelGGL((sos_serial_lds_kernel<S, C, I>), grid, dim3(64), 0, st, (const I*)a.x, (I*)a.y,
+                           (const C*)a.coefs, (const I*)a.st_in, (I*)a.st_out, (long long)a.n, (int)a.channels,
+                           vec_ok);
     } else {
         dim3 grid((unsigned)((a.channels + 63) / 64));
         hipLaunchKernelGGL((sos_serial_kernel<S, C, I>), grid, dim3(64), 0, st, (const I*)a.x, (I*)a.y,

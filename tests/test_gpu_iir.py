@@ -399,3 +399,20 @@ def test_normal_df2_wave_scan(dt, cdt, sdt, tol, order):
     if cdt == np.float32:  # a direct-form polynomial in f32: as accurate as the f32 reference loop
         tol = max(tol, 10 * rel_rms(O.iir(dt, b, a, O.NORMAL).execute_block(x), ref))
     assert rel_rms(y, ref) <= tol, (rel_rms(y, ref), tol)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", DT)
+@pytest.mark.parametrize("ch,n", [(64, 4096), (70, 1000), (130, 77)])
+def test_sos_serial_bank_lds_bit_parity(dt, cdt, sdt, ch, n):
+    """the LDS-staged serial kernel (banks of >= 64 channels): every channel bit-identical to
+    its own reference-order recurrence, over ragged calls (tile tails, unaligned lengths)"""
+    num, den = O.active_lag(*ACTIVE_LAG)
+    num, den = num.astype(cdt), den.astype(cdt)
+    rng = np.random.default_rng(ch + n + dt)
+    x = rand(rng, ch * n, sdt).reshape(ch, n)
+    f = IIRFilter(num, den, SO, sample_dtype=sdt, algo=sd.ALGO_EXACT, channels=ch)
+    cut = n // 3
+    y = np.concatenate([f.execute_block(np.ascontiguousarray(x[:, :cut])),
+                        f.execute_block(np.ascontiguousarray(x[:, cut:]))], axis=1)
+    for c in range(0, ch, 7):
+        assert bits_equal(y[c], O.iir(dt, num, den, O.SECOND_ORDER).execute_block(x[c])), c
