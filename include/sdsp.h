@@ -135,10 +135,13 @@ typedef enum {
     SDSP_TUNE_DECIM_SEG = 6,     /* FMA decimator: outputs per lane group (0 = automatic) */
     SDSP_TUNE_IIR_WAVE_SCAN = 7, /* IIR scan kernel: 0 = block scan, 1 (default) = wave scan with 256-byte chunks,
                                     2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */
-    SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: 1 (default) = streaming M=1024 kernel where it applies, 0 = per-frame */
+    SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: streaming M=1024 kernel where it applies, 2 (default) =
+                                     512-thread workgroups, 1 = 1024-thread workgroups; 0 = per-frame */
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
-    SDSP_TUNE_OLS_KERNEL = 14    /* overlap-save interior segments (16-byte aligned rows): 0 (default) one-shot
+    SDSP_TUNE_OLS_KERNEL = 14,   /* overlap-save interior segments (16-byte aligned rows): 0 (default) one-shot
                                     XCD-ordered kernel, 1 persistent packed kernel (L <= 1025), 2 scalar kernel */
+    SDSP_TUNE_CHAN_XCD_ORDER = 15 /* streaming channeliser: 1 (default) = each XCD walks a contiguous
+                                     eighth of the frame chunks, 0 = launch order */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */
@@ -308,7 +311,8 @@ SDSP_API int sdsp_chan_create(sdsp_chan** out, int dtype, const void* taps, size
                               int device);
 SDSP_API void sdsp_chan_destroy(sdsp_chan* h);
 SDSP_API int sdsp_chan_set_streams(sdsp_chan* h, size_t streams);
-/* kernel-variant knobs: SDSP_TUNE_CHAN_STREAMING, SDSP_TUNE_CHAN_FRAMES_PER_BLOCK (performance only) */
+/* kernel-variant knobs: SDSP_TUNE_CHAN_STREAMING, SDSP_TUNE_CHAN_FRAMES_PER_BLOCK,
+ * SDSP_TUNE_CHAN_XCD_ORDER (performance only) */
 SDSP_API int sdsp_chan_set_tuning(sdsp_chan* h, int key, int value);
 SDSP_API int sdsp_chan_reset(sdsp_chan* h);
 SDSP_API int sdsp_chan_execute_block(sdsp_chan* h, const void* in, size_t n, void* out, size_t* frames);

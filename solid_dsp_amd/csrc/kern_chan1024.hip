@@ -14,22 +14,24 @@
 //   * FFT: wave w transforms buffer w, 1024 = 16 x 16 x 4 with the
 //     decomposition n = n0 + 4 n1 + 64 n2, k = k2 + 16 k1 + 256 k0:
 //       P1 lane L = n0 + 4 n1: DFT16 over n2, * W1024^(L k2)
-//       P2 lane (n0, k2):      DFT16 over n1, * W1024^(16 n0 k1)
-//       P3 lane l, c = l + 64 j: DFT4 over n0 -> X[c + 256 k0] (coalesced stores)
-//     with two wave-local LDS transposes, so the four FFTs need no workgroup
-//     barrier.  Outputs: natural channel order, as kern_fft.hip.
+//       P2 lane k2 + 16 n0:    DFT16 over n1, * W1024^(16 n0 k1)
+//       P3 lanes (k2 + 16 n0), row-swap transposed: DFT4 over n0 -> X[k2 + 16 k1 + 256 k0]
+//     with one wave-local LDS transpose (swizzled, conflict-free; see
+//     fft1024_chan), so the FFTs need no workgroup barrier.  Outputs: natural
+//     channel order, as kern_fft.hip.
 // Arithmetic: fused multiply-add, f32; parity is the §8d tolerance against the
 // f64 restatement (tests/test_gpu_fft.py).
 #include "sdsp_device.hpp"
 #include <cstdlib>
 
 #include "sdsp_kernels.hpp"
+#include "sdsp_pk.hpp"
 
 namespace sdsp {
 
 namespace {
 
-struct cf { float re, im; };
+struct alignas(8) cf { float re, im; };  // 8-byte aligned: b64 LDS / global accesses
 __device__ __forceinline__ cf cadd(cf a, cf b) { return {a.re + b.re, a.im + b.im}; }
 __device__ __forceinline__ cf csub(cf a, cf b) { return {a.re - b.re, a.im - b.im}; }
 __device__ __forceinline__ cf cmul(cf a, cf b) {
@@ -91,15 +93,7 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void st_nt(cf* p, cf v) {  // one 8-byte streaming store
-    __builtin_nontemporal_store(f2v{v.re, v.im}, reinterpret_cast<f2v*>(p));
-}
-
 constexpr int kM = 1024;
-constexpr int kThreads = 1024;           // one branch per thread, 16 waves
-constexpr int kNB = kM / kThreads;       // branches per thread
-constexpr int kFrames = kThreads / 64;   // frames per round: one FFT per wave
 
 // Wave buffer: 64 rows of 18 complex (16 + 2 pad): every LDS address below is
 // a lane base plus a compile-time offset, and 16 lanes reading the same slot
@@ -134,26 +128,6 @@ __device__ __forceinline__ void fft1024_p12(cf* __restrict__ buf, const cf* __re
     wave_sync();
 }
 
-// one frame's FFT by one wave: buffer holds v[p] at index p on entry,
-// natural-order X written to yf
-__device__ __forceinline__ void fft1024_wave(cf* __restrict__ buf, const cf* __restrict__ stw, int L,
-                                             cf* __restrict__ yf, bool store) {
-    fft1024_p12(buf, stw, L);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int c = L + 64 * j;
-        cf a0 = buf[c * 4 + 0], a1 = buf[c * 4 + 1], a2 = buf[c * 4 + 2], a3 = buf[c * 4 + 3];
-        dft4(a0, a1, a2, a3);
-        if (store) {
-            st_nt(yf + c, a0);
-            st_nt(yf + c + 256, a1);
-            st_nt(yf + c + 512, a2);
-            st_nt(yf + c + 768, a3);
-        }
-    }
-    wave_sync();
-}
-
 // the same FFT leaving natural-order X in buf[0, 1024)
 __device__ __forceinline__ void fft1024_wave_lds(cf* __restrict__ buf, const cf* __restrict__ stw, int L) {
     fft1024_p12(buf, stw, L);
@@ -175,62 +149,197 @@ __device__ __forceinline__ void fft1024_wave_lds(cf* __restrict__ buf, const cf*
     wave_sync();
 }
 
-template <int K>
-__global__ void __launch_bounds__(kThreads)
-chan1024_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const float* __restrict__ cb,
-                cf* __restrict__ y, const cf* __restrict__ tw, long long n, long long frames, int F) {
-    __shared__ cf stw[kM];
-    __shared__ cf sbuf[kFrames * kBuf];
+// ---- the channeliser's per-frame FFT --------------------------------------
+// Same decomposition and arithmetic as fft1024_p12 + the DFT4 pass (bit for
+// bit), with fewer LDS cycles per frame:
+//   * frame buffer of 1024 complex, unpadded: the PFB writes v[p] at p (rows of
+//     512 B) and P1 reads v[L + 64 n2];
+//   * the P1 -> P2 transpose goes to 64 rows of 16 with column c of row r at
+//     r*16 + (c ^ swz(r)), swz(r) = ((r & 3) << 2) ^ (r >> 2): conflict-free for
+//     the P1 stores (16-lane groups see 16 distinct columns) and for the P2 reads
+//     (lane k2 + 16 n0 reads row n0 + 4 k2: 32-lane groups, row parity x column
+//     distinct);
+//   * twiddles from [k2][L] and [k1][n0] tables (contiguous / broadcast reads,
+//     where W^(L k2) from one 1024-entry table was up to 8-way bank-conflicted);
+//   * the final DFT4 over n0: a 4 x 4 lanes x registers transpose with the
+//     gfx950 row swaps (P2 puts n0 in lane bits 4-5), then in registers, instead
+//     of a third LDS round trip; stores stay 512 contiguous bytes in lane order.
+using pk::f2;
+
+struct ChanTw {
+    f2 p1[15 * 64];  // W^(L k2), k2 = 1..15
+    f2 p2[16 * 4];   // W^(16 n0 k1)
+};
+
+__device__ __forceinline__ void chan_tw_init(ChanTw& s, const f2* __restrict__ tw, int t, int nt) {
+    for (int i = t; i < 15 * 64; i += nt) s.p1[i] = tw[((i & 63) * ((i >> 6) + 1)) & (kM - 1)];
+    for (int i = t; i < 64; i += nt) s.p2[i] = tw[(16 * (i & 3) * (i >> 2)) & (kM - 1)];
+}
+
+// exchange between lane rows (gfx950 v_permlane16/32_swap): with S = 16 the odd
+// 16-lane rows of a trade places with the even rows of b, with S = 32 the upper
+// half of a with the lower half of b -- one step of a lanes x registers transpose
+template <int S> __device__ __forceinline__ void row_swap(float& a, float& b) {
+    const unsigned ua = __float_as_uint(a), ub = __float_as_uint(b);
+    auto r = S == 16 ? __builtin_amdgcn_permlane16_swap(ua, ub, false, false)
+                     : __builtin_amdgcn_permlane32_swap(ua, ub, false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+template <int S> __device__ __forceinline__ void row_swap(f2& a, f2& b) {
+    float ax = a.x, ay = a.y, bx = b.x, by = b.y;
+    row_swap<S>(ax, bx);
+    row_swap<S>(ay, by);
+    a = f2{ax, ay};
+    b = f2{bx, by};
+}
+
+__device__ __forceinline__ void st_nt2(f2* p, f2 v) { __builtin_nontemporal_store(v, p); }
+
+// one frame by one wave: buf holds v[p] at p; natural-order X to yf.  Packed
+// FP32 throughout (sdsp_pk.hpp: each complex add / multiply is one or two
+// v_pk_* instructions, the same per-component operation order as cmul / dft4 /
+// tw16 above); pdft16 leaves X[k] of its 16 points at v[kout(k)].
+__device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw& tw, int L, f2* __restrict__ yf,
+                                             bool store) {
+    using pk::kout;
+    // the swizzled addresses depend on the lane only: keep them from being
+    // hoisted out of the caller's frame loop (32 loop-invariant VGPRs spill)
+    asm volatile("" : "+v"(L));
+    f2 v[16];
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) v[n2] = buf[L + 64 * n2];
+    pk::pdft16<false>(v);
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) v[kout(k2)] = pk::pmul(v[kout(k2)], tw.p1[(k2 - 1) * 64 + L]);
+    wave_sync();
+    {
+        // P1 lane L = n0 + 4 n1 writes row r = n0 + 4 k2, column n1
+        const int n0 = L & 3, n1 = L >> 2;
+        const int u = n1 ^ (n0 << 2);  // swz(r) = (n0 << 2) ^ k2
+        f2* row = buf + n0 * 16;
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) row[64 * k2 + (u ^ k2)] = v[kout(k2)];
+    }
+    wave_sync();
+    // P2 lane L = k2 + 16 n0 reads row r = n0 + 4 k2 (n1 = 0..15)
+    const int n0 = L >> 4, k2 = L & 15;
+    {
+        const int sw = (n0 << 2) ^ k2;
+        const f2* row = buf + (n0 + 4 * k2) * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = row[i ^ sw];
+    }
+    pk::pdft16<false>(v);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) v[kout(k1)] = pk::pmul(v[kout(k1)], tw.p2[k1 * 4 + n0]);
+    if (!store) return;  // uniform over the wave
+    // P3: per block of four k1 = 4 b + i, transpose lanes n0 (lane bits 4, 5) x
+    // registers i, so lane (n0, k2) holds the four n0-inputs of k1 = 4 b + n0; an
+    // in-register DFT4 then gives X[k2 + 16 (4 b + n0) + 256 k0] = X[L + 64 b + 256 k0]:
+    // every store instruction writes 512 bytes in lane order (8-byte and paired
+    // 16-byte stores measured the same on cfg5)
+    f2* yl = yf + L;
+#pragma unroll
+    for (int bk = 0; bk < 4; ++bk) {
+        f2 r[4] = {v[kout(4 * bk)], v[kout(4 * bk + 1)], v[kout(4 * bk + 2)], v[kout(4 * bk + 3)]};
+        row_swap<16>(r[0], r[1]);
+        row_swap<16>(r[2], r[3]);
+        row_swap<32>(r[0], r[2]);
+        row_swap<32>(r[1], r[3]);
+        pk::pdft4<false>(r[0], r[1], r[2], r[3]);
+#pragma unroll
+        for (int k0 = 0; k0 < 4; ++k0) st_nt2(yl + 64 * bk + 256 * k0, r[k0]);
+    }
+}
+
+// T = 1024: one branch per thread, sixteen frames per round, 136 KB of LDS
+// (one workgroup per CU).  T = 512: two branches per thread, eight frames per
+// round, 72 KB (two workgroups per CU, so one's loads overlap the other's
+// PFB/FFT).  Twiddle tables in LDS for both.
+template <int K, int T>
+__global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD: 128 VGPRs
+chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
+                f2* __restrict__ y, const f2* __restrict__ tw, long long n, long long frames, int F, int cps,
+                int C, int xcd) {
+    constexpr int kThreads = T, kNB = kM / T, kFrames = T / 64;
+    __shared__ ChanTw stw;
+    __shared__ f2 sbuf[kFrames * kM];
     const int t = threadIdx.x, L = t & 63, w = t >> 6;
-    const int s = blockIdx.y;
+    // chunks of F frames, C in all (cps per stream), walked by G resident
+    // workgroups.  xcd: workgroup b runs on XCD b mod 8 (dispatch order), so XCD x
+    // takes the contiguous range [x Q, (x+1) Q) of chunks, Q = ceil(C / 8), and its
+    // G/8 workgroups step through it side by side: at any time an XCD streams one
+    // window of neighbouring chunks (DRAM row locality), and a chunk's K-1 warm-up
+    // frames were just read by the workgroup on the chunk before (same L2).
+    // Without xcd: chunk b + k G.
+    const unsigned G = gridDim.x, bid = blockIdx.x;
+#ifdef SDSP_CHAN_LAB
+    const int lab = xcd >> 4;  // ablations (tools/chan_ab.py): 1 no FFT, 2 no loads, 4 no stores
+    xcd &= 1;
+#else
+    constexpr int lab = 0;
+#endif
+    const unsigned Q = xcd ? (C + 7) / 8 : C, Gx = xcd ? G / 8 : G;
+    const unsigned c_lo = xcd ? (bid & 7) * Q : 0, c_hi = c_lo + Q < (unsigned)C ? c_lo + Q : C;
+    const unsigned c_first = c_lo + (xcd ? bid >> 3 : bid);
     const long long H = (long long)(K - 1) * kM;
     static_assert(kFrames % 8 == 0, "ring slots are frame mod 8");
-    x += (long long)s * n;
-    y += (long long)s * n;
-    hist += (long long)s * H;
-    const long long m0 = (long long)blockIdx.x * F;
-    const long long m_end = m0 + F < frames ? m0 + F : frames;
-    for (int i = t; i < kM; i += kThreads) stw[i] = tw[i];
+    const f2* __restrict__ xs = x;
+    const f2* __restrict__ hs = hist;
+    f2* __restrict__ ys = y;
+    long long m0 = 0, m_end = 0;
+    chan_tw_init(stw, tw, t, kThreads);
 
-    // branches p_j = t + kThreads j
+    // Branch taps are re-read (L2-resident, 32 KB)
+    // each round rather than held across the FFT: that keeps the FFT phase
+    // inside 128 VGPRs (four waves per SIMD).  The pointer goes through an
+    // empty asm so the loads stay inside the loop.
+    // branches of this thread: T = 1024: p = t; T = 512: p = 2t + j, whose samples
+    // x[f M + M-1-p] are adjacent -- one 16-byte load per frame (8-byte accesses
+    // stream at well under the 16-byte rate)
+    constexpr bool kPair = kNB == 2;
+    auto branch = [&](int j) { return kPair ? 2 * t + j : t + kThreads * j; };
+    auto load_pair = [&](const f2* xf, f2 (&v)[kNB]) {
+        if constexpr (kPair) {
+            const pk::f4v q = *reinterpret_cast<const pk::f4v*>(xf + kM - 2 - 2 * t);
+            v[0] = f2{q.z, q.w};  // branch 2t:   x[M-1-2t]
+            v[1] = f2{q.x, q.y};  // branch 2t+1: x[M-2-2t]
+        } else {
+            v[0] = xf[kM - 1 - t];
+        }
+    };
     float c[kNB][K];
+    auto load_taps = [&]() {
+        const float* cbp = cb;
+        asm volatile("" : "+s"(cbp));
 #pragma unroll
-    for (int j = 0; j < kNB; ++j)
+        for (int j = 0; j < kNB; ++j)
 #pragma unroll
-        for (int i = 0; i < K; ++i) c[j][i] = cb[(t + kThreads * j) * K + i];
-
-    // input sample of branch p_j at frame f: x[f*M + M-1-p_j]; before the call: history
-    auto ext = [&](long long f, int j) -> cf {
-        const long long q = f * kM + (kM - 1 - t - kThreads * j);
-        if (q >= 0) return q < n ? x[q] : cf{0.0f, 0.0f};
-        return H + q >= 0 ? hist[H + q] : cf{0.0f, 0.0f};
+            for (int i = 0; i < K; ++i) c[j][i] = cbp[branch(j) * K + i];
     };
 
-    cf ring[kNB][8];
-#pragma unroll
-    for (int j = 0; j < kNB; ++j)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) ring[j][r] = cf{0.0f, 0.0f};
-    // warm-up: frames m0-1 .. m0-K+1 into slots 7 .. 8-K+1 (slot = frame - m0 mod 8)
-#pragma unroll
-    for (int q = 1; q < K; ++q)
-#pragma unroll
-        for (int j = 0; j < kNB; ++j) ring[j][8 - q] = ext(m0 - q, j);
+    // input sample of branch p_j at frame f: x[f*M + M-1-p_j]; before the call: history
+    auto ext = [&](long long f, int j) -> f2 {
+        const long long q = f * kM + (kM - 1 - branch(j));
+        if (q >= 0) return q < n ? xs[q] : f2{0.0f, 0.0f};
+        return H + q >= 0 ? hs[H + q] : f2{0.0f, 0.0f};
+    };
+
+    f2 ring[kNB][8];
 
     // a round's new samples: plain loads when those frames exist (uniform test; a
     // per-load branch would serialise the HBM round trips), else guarded
-    // a round's new samples: plain loads when those frames exist (uniform test; a
-    // per-load branch would serialise the HBM round trips), else guarded
-    cf nx[kFrames][kNB];
+    f2 nx[kFrames][kNB];
     auto load_round = [&](long long f0) {
-        if (f0 + kFrames <= frames) {
-            const int off = kM - 1 - t;  // uniform frame base (SGPRs) + 32-bit lane offset
+        if (lab & 2) {
 #pragma unroll
-            for (int f = 0; f < kFrames; ++f) {
-                const cf* xf = x + (f0 + f) * kM;
+            for (int f = 0; f < kFrames; ++f)
 #pragma unroll
-                for (int j = 0; j < kNB; ++j) nx[f][j] = xf[off - kThreads * j];
-            }
+                for (int j = 0; j < kNB; ++j) nx[f][j] = ring[j][(f + 3) & 7];
+        } else if (f0 + kFrames <= frames) {
+#pragma unroll
+            for (int f = 0; f < kFrames; ++f) load_pair(xs + (f0 + f) * kM, nx[f]);
         } else {
 #pragma unroll
             for (int f = 0; f < kFrames; ++f)
@@ -240,28 +349,67 @@ chan1024_kernel(const cf* __restrict__ x, const cf* __restrict__ hist, const flo
     };
     __syncthreads();
 
-    for (long long mb = m0; mb < m_end; mb += kFrames) {
-        load_round(mb);
-        // PFB: frame mb + g into buffer g (ring slot g mod 8)
+    for (unsigned ck = c_first; ck < c_hi; ck += Gx) {
+        const int s = (int)(ck / cps);
+        xs = x + (long long)s * n;
+        ys = y + (long long)s * n;
+        hs = hist + (long long)s * H;
+        m0 = (long long)(ck - (unsigned)s * cps) * F;
+        m_end = m0 + F < frames ? m0 + F : frames;
 #pragma unroll
-        for (int g = 0; g < kFrames; ++g) {
+        for (int j = 0; j < kNB; ++j)
 #pragma unroll
-            for (int j = 0; j < kNB; ++j) {
-                ring[j][g & 7] = nx[g][j];
-                cf acc = {0.0f, 0.0f};
+            for (int r = 0; r < 8; ++r) ring[j][r] = f2{0.0f, 0.0f};
+        // warm-up: frames m0-1 .. m0-K+1 into slots 7 .. 8-K+1 (slot = frame - m0 mod 8)
+        if (m0 >= K - 1) {  // uniform: plain loads (all in flight together)
 #pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    const cf h = ring[j][(g - i) & 7];
-                    acc.re = __builtin_fmaf(c[j][i], h.re, acc.re);
-                    acc.im = __builtin_fmaf(c[j][i], h.im, acc.im);
-                }
-                sbuf[g * kBuf + t + kThreads * j] = acc;
+            for (int q = 1; q < K; ++q) {
+                f2 v[kNB];
+                load_pair(xs + (m0 - q) * kM, v);
+#pragma unroll
+                for (int j = 0; j < kNB; ++j) ring[j][8 - q] = v[j];
             }
+        } else {
+#pragma unroll
+            for (int q = 1; q < K; ++q)
+#pragma unroll
+                for (int j = 0; j < kNB; ++j) ring[j][8 - q] = ext(m0 - q, j);
         }
-        __syncthreads();
-        const long long f = mb + w;
-        fft1024_wave(sbuf + w * kBuf, stw, L, y + f * kM, f < m_end);
-        __syncthreads();
+        for (long long mb = m0; mb < m_end; mb += kFrames) {
+            load_taps();
+            load_round(mb);
+            // PFB: frame mb + g into buffer g (ring slot g mod 8); per component
+            // acc = fma(c_i, h, acc), one v_pk_fma_f32 per tap
+#pragma unroll
+            for (int g = 0; g < kFrames; ++g) {
+                f2 pacc[kNB];
+#pragma unroll
+                for (int j = 0; j < kNB; ++j) {
+                    ring[j][g & 7] = nx[g][j];
+                    f2 acc = {0.0f, 0.0f};
+#pragma unroll
+                    for (int i = 0; i < K; ++i)
+                        acc = __builtin_elementwise_fma(f2{c[j][i], c[j][i]}, ring[j][(g - i) & 7], acc);
+                    pacc[j] = acc;
+                }
+                if constexpr (kPair) {  // branches 2t, 2t+1: one 16-byte LDS store
+                    *reinterpret_cast<pk::f4v*>(sbuf + g * kM + 2 * t) = pk::f4v{pacc[0].x, pacc[0].y, pacc[1].x, pacc[1].y};
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kNB; ++j) sbuf[g * kM + t + kThreads * j] = pacc[j];
+                }
+            }
+            __syncthreads();
+            const long long f = mb + w;
+            if (lab & 1) {
+                if (!(lab & 4) && f < m_end)
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) st_nt2(ys + f * kM + L + 64 * k, sbuf[w * kM + L + 64 * k]);
+            } else {
+                fft1024_chan(sbuf + w * kM, stw, L, ys + f * kM, f < m_end && !(lab & 4));
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -343,26 +491,50 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 
 }  // namespace
 
+#ifdef SDSP_CHAN_LAB
+static int g_chan_lab = 0;
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) { g_chan_lab = v; }
+#endif
+
 // M = 1024, complex f32, K <= 8 taps per branch; false = not applicable
 bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
-    if (a.M != 1024 || a.K < 1 || a.K > 8) return false;
-    // frames per workgroup (multiple of kFrames): each workgroup re-reads K-1 warm-up frames
-    // default: as long as the grid keeps >= ~2 workgroups per CU (measured on cfg5: 64 -> 256
-    // frames per workgroup 0.525 -> 0.499 ms, warm-up traffic 11% -> 3%)
+    if (a.M != 1024 || a.K < 1 || a.K > 8 || a.fast <= 0) return false;
+    // the 512-thread form loads 16 bytes per lane: 1024-thread form for an input
+    // that is only 8-byte aligned
+    const int var = a.fast == 2 && ((uintptr_t)a.x & 15) ? 1 : a.fast;
+    // chunk of F frames (a whole number of rounds); each chunk re-reads K-1 warm-up
+    // frames (L2 hits when the neighbouring chunk is in flight on the same XCD)
+    const int R = var == 2 ? 8 : 16;  // frames per round
     long long Fd = (long long)(a.frames * a.streams) / 512;
     Fd = Fd < 64 ? 64 : (Fd > 256 ? 256 : Fd);
-    const int F = (int)(((a.frames_per_block > 0 ? a.frames_per_block : Fd) + kFrames - 1) / kFrames * kFrames);
-    static_assert(64 % kFrames == 0, "F");
-    dim3 grid((unsigned)((a.frames + F - 1) / F), (unsigned)a.streams);
-#define SDSP_CHAN(KV)                                                                                          \
-    case KV:                                                                                                   \
-        hipLaunchKernelGGL((chan1024_kernel<KV>), grid, dim3(kThreads), 0, s, (const cf*)a.x, (const cf*)a.hist,    \
-                           (const float*)a.cb, (cf*)a.y, (const cf*)a.tw, (long long)a.n, (long long)a.frames, F); \
+    const int F = (int)(((a.frames_per_block > 0 ? a.frames_per_block : Fd) + R - 1) / R * R);
+    const long long cps = ((long long)a.frames + F - 1) / F, C = cps * (long long)a.streams;
+    if (C > (1LL << 30)) return false;
+    // resident workgroups: 256 CUs x (2 of 512 threads | 1 of 1024)
+    const long long resident = var == 2 ? 512 : 256;
+    int xcd = a.xcd_order ? 1 : 0;
+    long long G = C < resident ? C : resident;
+    if (xcd) {
+        G = G / 8 * 8;  // whole workgroups per XCD
+        if (G == 0) xcd = 0, G = C;
+    }
+    dim3 grid((unsigned)G);
+#ifdef SDSP_CHAN_LAB
+    xcd |= g_chan_lab << 4;
+#endif
+#define SDSP_CHAN_T(KV, T)                                                                                 \
+    hipLaunchKernelGGL((chan1024_kernel<KV, T>), grid, dim3(T), 0, s, (const f2*)a.x, (const f2*)a.hist,     \
+                       (const float*)a.cb, (f2*)a.y, (const f2*)a.tw, (long long)a.n, (long long)a.frames, F, (int)cps, \
+                       (int)C, xcd)
+#define SDSP_CHAN(KV)                                                                      \
+    case KV:                                                                               \
+        if (var == 2) SDSP_CHAN_T(KV, 512); else SDSP_CHAN_T(KV, 1024);                 \
         break;
     switch (a.K) {
         SDSP_CHAN(1) SDSP_CHAN(2) SDSP_CHAN(3) SDSP_CHAN(4) SDSP_CHAN(5) SDSP_CHAN(6) SDSP_CHAN(7) SDSP_CHAN(8)
     }
 #undef SDSP_CHAN
+#undef SDSP_CHAN_T
     *err = hipGetLastError();
     return true;
 }

@@ -340,7 +340,7 @@ hipError_t launch_chan_t(const ChanArgs& a, hipStream_t s) {
 hipError_t launch_chan(bool f64, const ChanArgs& a, hipStream_t s) {
     if (a.frames == 0) return hipSuccess;
     hipError_t err;
-    if (!f64 && a.fast && try_launch_chan1024(a, s, &err)) return err;
+    if (!f64 && try_launch_chan1024(a, s, &err)) return err;
     return f64 ? launch_chan_t<double>(a, s) : launch_chan_t<float>(a, s);
 }
 

@@ -192,8 +192,9 @@ struct sdsp_chan {
     std::vector<unsigned char> taps;
     DevBuf cb, tw, hist[2], stage_in, stage_out;
     int cur = 0;
-    bool fast = true;  // streaming M = 1024 kernel (SDSP_TUNE_CHAN_STREAMING)
+    int fast = 2;  // streaming M = 1024 kernel variant (SDSP_TUNE_CHAN_STREAMING)
     int fpb = 0;       // its frames per workgroup (SDSP_TUNE_CHAN_FRAMES_PER_BLOCK, 0 = default)
+    bool xcd = true;   // XCD-contiguous chunk order (SDSP_TUNE_CHAN_XCD_ORDER)
     hipStream_t stream = nullptr;
 };
 
@@ -400,8 +401,9 @@ int sdsp_chan_set_streams(sdsp_chan* h, size_t streams) {
 
 int sdsp_chan_set_tuning(sdsp_chan* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
-    if (key == SDSP_TUNE_CHAN_STREAMING) h->fast = value != 0;
+    if (key == SDSP_TUNE_CHAN_STREAMING && value >= 0 && value <= 2) h->fast = value;
     else if (key == SDSP_TUNE_CHAN_FRAMES_PER_BLOCK && value >= 0) h->fpb = value;
+    else if (key == SDSP_TUNE_CHAN_XCD_ORDER) h->xcd = value != 0;
     else return SDSP_E_INVALID_ARGUMENT;
     return SDSP_OK;
 }
@@ -423,6 +425,7 @@ int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, voi
     ChanArgs a{d_in, h->hist[h->cur].p, h->cb.p, d_out, h->tw.p, (int)h->M, ilog2(h->M), (int)h->K, n, fr, h->streams};
     a.fast = h->fast;
     a.frames_per_block = h->fpb;
+    a.xcd_order = h->xcd;
     F_TRY(launch_chan(h->dtype == SDSP_RC64, a, s), "channeliser");
     const int H = (int)((h->K - 1) * h->M);
     F_TRY(launch_hist_update(h->dtype, d_in, h->hist[h->cur].p, h->hist[h->cur ^ 1].p, n, H, h->streams, s),

@@ -153,8 +153,9 @@ struct ChanArgs {
     const void* tw;
     int M, logM, K;
     size_t n, frames, streams;
-    bool fast = true;  // use the streaming kernel where it applies (sdsp_chan_set_tuning)
+    int fast = 2;  // streaming kernel where it applies: 0 off, 1 = 1024-thread, 2 = 512-thread (sdsp_chan_set_tuning)
     int frames_per_block = 0;  // streaming kernel: frames per workgroup (0 = default)
+    bool xcd_order = true;     // streaming kernel: XCD-contiguous chunk order
 };
 hipError_t launch_chan(bool f64, const ChanArgs& a, hipStream_t s);
 // streaming M = 1024 kernel (kern_chan1024.hip); false = not applicable

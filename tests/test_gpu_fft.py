@@ -102,6 +102,58 @@ def test_channelizer_multistream_device():
         assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-7
 
 
+@pytest.mark.parametrize("variant,fpb", [(0, 0), (1, 16), (1, 0), (2, 8), (2, 48)])
+@pytest.mark.parametrize("K", [3, 8])
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_channelizer_1024_streaming_variants(variant, fpb, K, xcd):
+    """the streaming M=1024 kernels (1024- and 512-thread workgroups, SDSP_TUNE_CHAN_STREAMING
+    1/2) and the per-frame kernel (0) against the restatement: several streams, workgroup
+    boundaries inside a block (warm-up frames), a ragged last round, two blocks (history),
+    launch-order and XCD-ordered chunk maps"""
+    import torch
+    M, S, frames = 1024, 4, 75
+    h = O.firdes_kaiser(M * K, 0.5 / M, 80.0, 0.0).astype(np.float32)
+    x = np.stack([O.synth(31, s, 0, M * frames, complex_=True) for s in range(S)]).astype(np.complex64)
+    ch = Channelizer(h, M, sample_dtype=np.complex64, streams=S)
+    assert sd.lib().sdsp_chan_set_tuning(ch._h, 8, variant) == 0
+    assert sd.lib().sdsp_chan_set_tuning(ch._h, 9, fpb) == 0
+    assert sd.lib().sdsp_chan_set_tuning(ch._h, 15, xcd) == 0
+    st = torch.cuda.current_stream()
+    y = np.zeros((S, frames, M), np.complex64)
+    for a, b in ((0, 32), (32, frames)):
+        d_in = to_dev(np.ascontiguousarray(x[:, a * M:b * M]).reshape(-1))
+        d_out = empty_dev(S * M * (b - a), np.complex64)
+        assert ch.execute_block_device(d_in, M * (b - a), d_out, st) == b - a
+        y[:, a:b] = to_host(d_out).reshape(S, b - a, M)
+    for s in range(S):
+        ref = np.zeros(M * frames, np.complex128)
+        O.lib().orc_channelize(O._ptr(h.astype(np.float64)), len(h), M, O._ptr(x[s].astype(np.complex128)),
+                               M * frames, O._ptr(ref))
+        assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-6
+
+
+@pytest.mark.parametrize("variant,fpb", [(1, 16), (2, 8)])
+@pytest.mark.parametrize("xcd", [0, 1])
+def test_channelizer_1024_persistent_chunk_walk(variant, fpb, xcd):
+    """more chunks than resident workgroups: every workgroup walks several chunks
+    (per-XCD windows or launch order), each restarting its PFB ring from K-1 warm-up frames"""
+    import torch
+    M, K, S, frames = 1024, 8, 2, 2100
+    h = O.firdes_kaiser(M * K, 0.5 / M, 80.0, 0.0).astype(np.float32)
+    x = np.stack([O.synth(77, s, 0, M * frames, complex_=True) for s in range(S)]).astype(np.complex64)
+    ch = Channelizer(h, M, sample_dtype=np.complex64, streams=S)
+    for key, v in ((8, variant), (9, fpb), (15, xcd)):
+        assert sd.lib().sdsp_chan_set_tuning(ch._h, key, v) == 0
+    d_out = empty_dev(S * M * frames, np.complex64)
+    assert ch.execute_block_device(to_dev(x.reshape(-1)), M * frames, d_out, torch.cuda.current_stream()) == frames
+    y = to_host(d_out).reshape(S, frames, M)
+    for s in range(S):
+        ref = np.zeros(M * frames, np.complex128)
+        O.lib().orc_channelize(O._ptr(h.astype(np.float64)), len(h), M, O._ptr(x[s].astype(np.complex128)),
+                               M * frames, O._ptr(ref))
+        assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-6
+
+
 @pytest.mark.parametrize("cdt,sdt,kind", [(np.float64, np.float64, 0), (np.float64, np.complex128, 1),
                                           (np.complex128, np.complex128, 2)])
 @pytest.mark.parametrize("direction", [Direction.FORWARD, Direction.REVERSE])

@@ -1,5 +1,6 @@
 """Interleaved in-process A/B of the channeliser kernels (per-frame chan_kernel vs
-the streaming M=1024 kernel, SDSP_TUNE_CHAN_STREAMING) on the cfg5 workload."""
+the streaming M=1024 kernels, SDSP_TUNE_CHAN_STREAMING 1 = 1024-thread, 2 = 512-thread) on the cfg5 workload.
+  CHAN_CASES="variant:frames_per_block:xcd_order,..." python tools/chan_ab.py"""
 import json
 import os
 import sys
@@ -9,8 +10,13 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(rounds=6):
+def main(rounds=9):
     import torch
+    lab = os.environ.get("CHAN_LAB")  # ablation bits per case (lab build): 1 no FFT, 2 no loads, 4 no stores
+    if lab:
+        import solid_dsp_amd._lib as LL
+        LL.LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "_build",
+                                   "libsdsp_lab.so")
     import solid_dsp_amd as sd
     from solid_dsp_amd import Channelizer
     from solid_dsp_amd.filter import firdes
@@ -21,23 +27,40 @@ def main(rounds=6):
         sd.lib().sdsp_synth_f32_device(d_in[s_ * n:].data_ptr(), 20250226, s_, 0, 2 * n, None)
     st = torch.cuda.current_stream()
     variants, outs = {}, {}
-    for fast, fpb in ((0, 0), (1, 32), (1, 64), (1, 128), (1, 256)):
+    cases = os.environ.get("CHAN_CASES", "0:0:0,1:256:0,1:256:1,2:256:1")
+    labs = {}
+    for c in cases.split(","):
+        fast, fpb, xcd, ab = ((int(v) for v in c.split(":")) if c.count(":") == 3 else
+                              (*(int(v) for v in c.split(":")), 0))
         f = Channelizer(h, M, sample_dtype=np.complex64, streams=S)
         assert sd.lib().sdsp_chan_set_tuning(f._h, 8, fast) == 0
         assert sd.lib().sdsp_chan_set_tuning(f._h, 9, fpb) == 0
-        key = f"fast{fast}_fpb{fpb}"
+        assert sd.lib().sdsp_chan_set_tuning(f._h, 15, xcd) == 0
+        key = f"fast{fast}_fpb{fpb}_xcd{xcd}" + (f"_lab{ab}" if ab else "")
+        labs[key] = ab
         variants[key] = f
+        if lab:
+            sd.lib().sdsp_lab_set_chan_ablation(ab)
         o = torch.empty_like(d_in)
         f.execute_block_device(d_in, n, o, st)
         torch.cuda.synchronize()
         outs[key] = o.cpu().numpy().astype(np.complex128)
         f.reset()
-    a = outs["fast0_fpb0"]
+    a = next(iter(outs.values()))
     agree = {k: float(np.linalg.norm(a - b) / np.linalg.norm(a)) for k, b in outs.items()}
     d_out = torch.empty_like(d_in)
     times = {k: [] for k in variants}
+    keys = list(variants)
+    if lab:
+        sd.lib().sdsp_lab_set_chan_ablation(0)
+    for _ in range(30):  # clocks settle
+        variants[keys[-1]].execute_block_device(d_in, n, d_out, st)
+    rng = np.random.default_rng(0)
     for _ in range(rounds):
-        for k, f in variants.items():
+        for k in rng.permutation(keys):
+            f = variants[k]
+            if lab:
+                sd.lib().sdsp_lab_set_chan_ablation(labs[k])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             f.execute_block_device(d_in, n, d_out, st)
