@@ -196,6 +196,7 @@ struct sdsp_chan {
     int fpb = 0;       // its frames per workgroup (SDSP_TUNE_CHAN_FRAMES_PER_BLOCK, 0 = default)
     bool xcd = true;   // XCD-contiguous chunk order (SDSP_TUNE_CHAN_XCD_ORDER)
     hipStream_t stream = nullptr;
+    StreamFence fence;  // last caller stream an execute call was queued on
 };
 
 extern "C" {
@@ -378,6 +379,7 @@ void sdsp_chan_destroy(sdsp_chan* h) {
     if (!h) return;
     {
         Guard g(h->device);
+        (void)h->fence.wait();
         if (h->stream) { (void)hipStreamSynchronize(h->stream); (void)hipStreamDestroy(h->stream); }
         h->cb.release(); h->tw.release(); h->hist[0].release(); h->hist[1].release();
         h->stage_in.release(); h->stage_out.release();
@@ -388,6 +390,7 @@ void sdsp_chan_destroy(sdsp_chan* h) {
 int sdsp_chan_set_streams(sdsp_chan* h, size_t streams) {
     if (!h || streams == 0) return SDSP_E_INVALID_ARGUMENT;
     Guard g(h->device);
+    F_TRY(h->fence.wait(), "wait for queued work");  // a queued block may still read the history
     h->streams = streams;
     const size_t hb = streams * (h->K - 1) * h->M * sample_bytes(h->dtype);
     for (int i = 0; i < 2; ++i) {
@@ -420,6 +423,11 @@ int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, voi
     const size_t fr = n / h->M;
     if (frames) *frames = fr;
     if (fr == 0) return SDSP_OK;
+    const size_t bytes = h->streams * n * sample_bytes(h->dtype);
+    if (ranges_overlap(d_in, bytes, d_out, bytes)) {
+        set_error("input and output blocks overlap (in-place channelising is not supported)");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
     Guard g(h->device);
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     ChanArgs a{d_in, h->hist[h->cur].p, h->cb.p, d_out, h->tw.p, (int)h->M, ilog2(h->M), (int)h->K, n, fr, h->streams};
@@ -431,6 +439,7 @@ int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, voi
     F_TRY(launch_hist_update(h->dtype, d_in, h->hist[h->cur].p, h->hist[h->cur ^ 1].p, n, H, h->streams, s),
           "history update");
     h->cur ^= 1;
+    if (s != h->stream) F_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 
@@ -457,6 +466,7 @@ int sdsp_chan_execute_block(sdsp_chan* h, const void* in, size_t n, void* out, s
 int sdsp_chan_synchronize(sdsp_chan* h) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     Guard g(h->device);
+    F_TRY(h->fence.wait(), "wait for queued work");
     F_TRY(hipStreamSynchronize(h->stream), "sync");
     return SDSP_OK;
 }

@@ -105,6 +105,7 @@ struct sdsp_iir {
     int algo = SDSP_ALGO_EXACT;  // reference-order recurrence unless the caller opts in (sdsp.h)
     int wscan = 1;  // 0: block scan; 1-4: wave-scan variant 0-3 (kern_iir_wscan.hip; sdsp_iir_set_tuning)
     hipStream_t stream = nullptr;
+    mutable StreamFence fence;  // last caller stream an execute call was queued on
     DevBuf stage_in, stage_out;
     size_t state_per_ch() const { return type == 1 ? (size_t)(2 * S) : (size_t)(cap - 1); }
 };
@@ -129,6 +130,7 @@ void push_coef(std::vector<unsigned char>& out, double v, int dt) {
 }
 
 int iir_alloc_state(sdsp_iir* h) {
+    IIR_TRY(h->fence.wait(), "wait for queued work");
     const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
     for (int i = 0; i < 2; ++i) {
         IIR_TRY(h->d_state[i].ensure(sb), "alloc state");
@@ -512,6 +514,7 @@ void sdsp_iir_destroy(sdsp_iir* h) {
     if (!h) return;
     {
         DeviceGuardI g(h->device);
+        (void)h->fence.wait();
         if (h->stream) {
             (void)hipStreamSynchronize(h->stream);
             (void)hipStreamDestroy(h->stream);
@@ -543,6 +546,7 @@ int sdsp_iir_clone(const sdsp_iir* h, sdsp_iir** out) {
         st = sdsp_iir_set_channels(c, h->channels);
         if (st) return st;
     }
+    IIR_TRY(h->fence.wait(), "wait for queued work");
     IIR_TRY(hipStreamSynchronize(h->stream), "sync");
     const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
     if (sb) IIR_TRY(hipMemcpy(c->d_state[0].p, h->d_state[h->cur].p, sb, hipMemcpyDeviceToDevice), "clone state");
@@ -603,6 +607,11 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
     const size_t nout = sdsp_iir_output_count(h, n);
     if (n_out) *n_out = nout;
     if (n == 0) return SDSP_OK;
+    if (ranges_overlap(d_in, h->channels * n * sample_bytes(h->dtype), d_out,
+                       h->channels * nout * sample_bytes(h->dtype))) {
+        set_error("input and output blocks overlap (in-place filtering is not supported)");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
     const int Mi = h->mode == 2 ? (int)h->M : 1;
     const int Md = h->mode == 1 ? (int)h->M : 1;
     const size_t nd = n * Mi;
@@ -682,6 +691,7 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
     }
     h->cur ^= 1;
     if (h->mode == 1) h->phase = (h->phase + nd) % h->M;
+    if (s != h->stream) IIR_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 
@@ -718,6 +728,7 @@ size_t sdsp_iir_state_len(const sdsp_iir* h) { return h ? h->channels * h->state
 int sdsp_iir_get_state(const sdsp_iir* h, void* state, size_t* phase) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuardI g(h->device);
+    IIR_TRY(h->fence.wait(), "wait for queued work");
     IIR_TRY(hipStreamSynchronize(h->stream), "sync");
     const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
     if (state && sb) IIR_TRY(hipMemcpy(state, h->d_state[h->cur].p, sb, hipMemcpyDeviceToHost), "get state");
@@ -728,6 +739,7 @@ int sdsp_iir_get_state(const sdsp_iir* h, void* state, size_t* phase) {
 int sdsp_iir_set_state(sdsp_iir* h, const void* state, size_t phase) {
     if (!h || phase >= h->M) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuardI g(h->device);
+    IIR_TRY(h->fence.wait(), "wait for queued work");
     IIR_TRY(hipStreamSynchronize(h->stream), "sync");
     const size_t sb = sample_bytes(h->dtype) * h->channels * h->state_per_ch();
     if (state && sb) IIR_TRY(hipMemcpy(h->d_state[h->cur].p, state, sb, hipMemcpyHostToDevice), "set state");
@@ -815,6 +827,7 @@ int sdsp_sos_section_coefs(const sdsp_iir* h, int section, double* num2, double*
 int sdsp_iir_synchronize(sdsp_iir* h) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuardI g(h->device);
+    IIR_TRY(h->fence.wait(), "wait for queued work");
     IIR_TRY(hipStreamSynchronize(h->stream), "sync");
     return SDSP_OK;
 }

@@ -190,3 +190,23 @@ def test_dot_product_batched_device_f32():
 
 def test_dot_product_kat():  # src/dot_product/mod.rs:15
     assert DotProduct(np.array([1.0, 2, 3, 4, 5]), Direction.REVERSE).execute(np.ones(5)) == 15.0
+
+
+def test_channelizer_rejects_in_place_and_orders_side_stream_reset():
+    import torch
+    M, K, frames = 1024, 8, 64
+    h = O.firdes_kaiser(M * K, 0.5 / M, 80.0, 0.0).astype(np.float32)
+    x = O.synth(12, 0, 0, M * frames, complex_=True).astype(np.complex64)
+    ch = Channelizer(h, M, sample_dtype=np.complex64)
+    buf = to_dev(np.concatenate([x, x]))
+    with pytest.raises(sd.SdspError) as e:
+        ch.execute_block_device(buf, M * frames, buf[M:])
+    assert e.value.code == 90
+    s = torch.cuda.Stream()
+    outs = [empty_dev(M * frames, np.complex64) for _ in range(2)]
+    with torch.cuda.stream(s):
+        ch.execute_block_device(buf[:M * frames], M * frames, outs[0], s)
+        ch.reset()  # must wait for the queued block before zeroing the history
+        ch.execute_block_device(buf[:M * frames], M * frames, outs[1], s)
+    torch.cuda.synchronize()
+    assert bits_equal(to_host(outs[0]), to_host(outs[1]))

@@ -416,3 +416,31 @@ def test_sos_serial_bank_lds_bit_parity(dt, cdt, sdt, ch, n):
                         f.execute_block(np.ascontiguousarray(x[:, cut:]))], axis=1)
     for c in range(0, ch, 7):
         assert bits_equal(y[c], O.iir(dt, num, den, O.SECOND_ORDER).execute_block(x[c])), c
+
+
+def test_iir_rejects_in_place_and_orders_side_stream_state():
+    """in-place device calls are refused; get_state / clone / reset wait for a
+    block queued on a caller stream (handle's own stream left idle)"""
+    import torch
+    from gpu_util import to_dev, empty_dev, to_host
+    b, a = butter()
+    n = 1 << 22
+    x = O.synth(6, 1, 0, n, complex_=False).astype(np.float32)
+    f = IIRFilter(b.astype(np.float32), a.astype(np.float32), SO, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+    buf = to_dev(np.concatenate([x, x]))
+    with pytest.raises(sd.SdspError) as e:
+        f.execute_block_device(buf, n, buf[n // 2:])
+    assert e.value.code == 90
+    s = torch.cuda.Stream()
+    out = empty_dev(n, np.float32)
+    with torch.cuda.stream(s):
+        f.execute_block_device(buf[:n], n, out, s)
+        st, _ = f.get_state()
+        g = f.clone()
+    torch.cuda.synchronize()
+    ref = IIRFilter(b.astype(np.float32), a.astype(np.float32), SO, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+    r = ref.execute_block(x)
+    rst, _ = ref.get_state()
+    assert bits_equal(to_host(out), r) and bits_equal(st, rst)
+    tail = x[:5000]
+    assert bits_equal(g.execute_block(tail), ref.execute_block(tail))
