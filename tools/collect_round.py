@@ -12,9 +12,10 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = {2: ("fir_ols4096_pk_kernel", "fft"), 3: ("sos_wscan_kernel", "scan"),
+KERNEL = {2: ("fir_ols_os", "fft"), 3: ("sos_wscan", "scan"),
           4: ("decim_poly_kernel", "fma"), 5: ("chan1024_kernel", "chan"),
-          6: ("acorr_kernel", "acorr"), 7: ("nco_mix_kernel", "nco"), 9: ("agc_kernel", "agc")}
+          6: ("acorr_kernel", "acorr"), 7: ("nco_mix_kernel", "nco"), 9: ("agc_kernel", "agc"),
+          10: ("interp_tile", "interp"), 11: ("sos_serial", "iir_serial_bank"), 12: ("sos_wscan", "normal_scan")}
 
 
 def main():
@@ -34,6 +35,9 @@ def main():
         stats = os.path.join(g, f"{a.tag}_prof_cfg{c}", "run_kernel_stats.csv")
         if os.path.exists(stats):
             shutil.copy(stats, os.path.join(a.out, f"kernel_stats_cfg{c}.csv"))
+        timed = os.path.join(g, f"{a.tag}_kernel_timed_cfg{c}.json")
+        if os.path.exists(timed):
+            shutil.copy(timed, os.path.join(a.out, f"kernel_timed_cfg{c}.json"))
         fetch = os.path.join(g, f"{a.tag}_pmc_fetch_cfg{c}")
         write = os.path.join(g, f"{a.tag}_pmc_write_cfg{c}")
         if c in KERNEL and os.path.isdir(fetch) and os.path.isdir(write):
