@@ -256,8 +256,12 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // T = 1024: one branch per thread, sixteen frames per round, 136 KB of LDS
 // (one workgroup per CU).  T = 512: two branches per thread, eight frames per
 // round, 72 KB (two workgroups per CU, so one's loads overlap the other's
-// PFB/FFT).  Twiddle tables in LDS for both.
-template <int K, int T>
+// PFB/FFT).  Twiddle tables in LDS for both.  PF (the default with T = 1024):
+// the next round's loads are issued after the PFB, before the FFT's stores --
+// vmcnt counts loads and stores in issue order, so loads issued after the
+// stores would make every round wait for the previous round's stores
+// (cfg5: 0.423 -> 0.414 ms against the 512-thread form, 25-round A/B).
+template <int K, int T, bool PF>
 __global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD: 128 VGPRs
 chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
                 f2* __restrict__ y, const f2* __restrict__ tw, long long n, long long frames, int F, int cps,
@@ -375,9 +379,13 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
 #pragma unroll
                 for (int j = 0; j < kNB; ++j) ring[j][8 - q] = ext(m0 - q, j);
         }
+        // PF: the next round's samples are requested before this round's FFT stores,
+        // so waiting for them (vmcnt counts loads and stores in issue order) never
+        // waits for the stores
+        if (PF) load_round(m0);
         for (long long mb = m0; mb < m_end; mb += kFrames) {
             load_taps();
-            load_round(mb);
+            if (!PF) load_round(mb);
             // PFB: frame mb + g into buffer g (ring slot g mod 8); per component
             // acc = fma(c_i, h, acc), one v_pk_fma_f32 per tap
 #pragma unroll
@@ -399,6 +407,7 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
                     for (int j = 0; j < kNB; ++j) sbuf[g * kM + t + kThreads * j] = pacc[j];
                 }
             }
+            if (PF && mb + kFrames < m_end) load_round(mb + kFrames);
             __syncthreads();
             const long long f = mb + w;
             if (lab & 1) {
@@ -501,17 +510,17 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
     if (a.M != 1024 || a.K < 1 || a.K > 8 || a.fast <= 0) return false;
     // the 512-thread form loads 16 bytes per lane: 1024-thread form for an input
     // that is only 8-byte aligned
-    const int var = a.fast == 2 && ((uintptr_t)a.x & 15) ? 1 : a.fast;
+    const int var = (a.fast == 2 || a.fast == 4) && ((uintptr_t)a.x & 15) ? 1 : a.fast;
     // chunk of F frames (a whole number of rounds); each chunk re-reads K-1 warm-up
     // frames (L2 hits when the neighbouring chunk is in flight on the same XCD)
-    const int R = var == 2 ? 8 : 16;  // frames per round
+    const int R = var == 2 || var == 4 ? 8 : 16;  // frames per round
     long long Fd = (long long)(a.frames * a.streams) / 512;
     Fd = Fd < 64 ? 64 : (Fd > 256 ? 256 : Fd);
     const int F = (int)(((a.frames_per_block > 0 ? a.frames_per_block : Fd) + R - 1) / R * R);
     const long long cps = ((long long)a.frames + F - 1) / F, C = cps * (long long)a.streams;
     if (C > (1LL << 30)) return false;
     // resident workgroups: 256 CUs x (2 of 512 threads | 1 of 1024)
-    const long long resident = var == 2 ? 512 : 256;
+    const long long resident = var == 2 || var == 4 ? 512 : 256;
     int xcd = a.xcd_order ? 1 : 0;
     long long G = C < resident ? C : resident;
     if (xcd) {
@@ -522,13 +531,16 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
 #ifdef SDSP_CHAN_LAB
     xcd |= g_chan_lab << 4;
 #endif
-#define SDSP_CHAN_T(KV, T)                                                                                 \
-    hipLaunchKernelGGL((chan1024_kernel<KV, T>), grid, dim3(T), 0, s, (const f2*)a.x, (const f2*)a.hist,     \
+#define SDSP_CHAN_T(KV, T, PF)                                                                             \
+    hipLaunchKernelGGL((chan1024_kernel<KV, T, PF>), grid, dim3(T), 0, s, (const f2*)a.x, (const f2*)a.hist,     \
                        (const float*)a.cb, (f2*)a.y, (const f2*)a.tw, (long long)a.n, (long long)a.frames, F, (int)cps, \
                        (int)C, xcd)
 #define SDSP_CHAN(KV)                                                                      \
     case KV:                                                                               \
-        if (var == 2) SDSP_CHAN_T(KV, 512); else SDSP_CHAN_T(KV, 1024);                 \
+        if (var == 2) SDSP_CHAN_T(KV, 512, false);                                         \
+        else if (var == 3) SDSP_CHAN_T(KV, 1024, true);                                    \
+        else if (var == 4) SDSP_CHAN_T(KV, 512, true);                                     \
+        else SDSP_CHAN_T(KV, 1024, false);                 \
         break;
     switch (a.K) {
         SDSP_CHAN(1) SDSP_CHAN(2) SDSP_CHAN(3) SDSP_CHAN(4) SDSP_CHAN(5) SDSP_CHAN(6) SDSP_CHAN(7) SDSP_CHAN(8)

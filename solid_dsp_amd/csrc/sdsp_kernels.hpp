@@ -153,7 +153,7 @@ struct ChanArgs {
     const void* tw;
     int M, logM, K;
     size_t n, frames, streams;
-    int fast = 2;  // streaming kernel where it applies: 0 off, 1 = 1024-thread, 2 = 512-thread (sdsp_chan_set_tuning)
+    int fast = 3;  // streaming kernel where it applies: 0 off, 1/3 = 1024-thread, 2/4 = 512-thread, 3/4 prefetching (sdsp_chan_set_tuning)
     int frames_per_block = 0;  // streaming kernel: frames per workgroup (0 = default)
     bool xcd_order = true;     // streaming kernel: XCD-contiguous chunk order
 };

@@ -102,7 +102,7 @@ def test_channelizer_multistream_device():
         assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-7
 
 
-@pytest.mark.parametrize("variant,fpb", [(0, 0), (1, 16), (1, 0), (2, 8), (2, 48)])
+@pytest.mark.parametrize("variant,fpb", [(0, 0), (1, 16), (1, 0), (2, 8), (2, 48), (3, 16), (3, 0), (4, 8), (4, 48)])
 @pytest.mark.parametrize("K", [3, 8])
 @pytest.mark.parametrize("xcd", [0, 1])
 def test_channelizer_1024_streaming_variants(variant, fpb, K, xcd):
@@ -132,7 +132,7 @@ def test_channelizer_1024_streaming_variants(variant, fpb, K, xcd):
         assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-6
 
 
-@pytest.mark.parametrize("variant,fpb", [(1, 16), (2, 8)])
+@pytest.mark.parametrize("variant,fpb", [(1, 16), (2, 8), (3, 16), (4, 8)])
 @pytest.mark.parametrize("xcd", [0, 1])
 def test_channelizer_1024_persistent_chunk_walk(variant, fpb, xcd):
     """more chunks than resident workgroups: every workgroup walks several chunks

@@ -10,7 +10,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(rounds=9):
+def main(rounds=int(os.environ.get("CHAN_ROUNDS", "9"))):
     import torch
     lab = os.environ.get("CHAN_LAB")  # ablation bits per case (lab build): 1 no FFT, 2 no loads, 4 no stores
     if lab:

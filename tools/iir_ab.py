@@ -12,6 +12,9 @@ sys.path.insert(0, REPO)
 
 def main(rounds=8, log2n=30):
     import torch
+    if os.environ.get("IIR_LIB"):  # e.g. tools/_build/libsdsp_lab.so: an older build, same box
+        import solid_dsp_amd._lib as LL
+        LL.LIB_PATH = os.path.join(REPO, os.environ["IIR_LIB"])
     import solid_dsp_amd as sd
     from solid_dsp_amd import IIRFilter, IIRFilterType
     n = 1 << log2n
@@ -22,7 +25,7 @@ def main(rounds=8, log2n=30):
     sd.lib().sdsp_synth_f32_device(d_in.data_ptr(), 20250226, 0, 0, n, None)
     s = torch.cuda.current_stream()
     variants, outs = {}, {}
-    for ws in (0, 1, 2, 5):
+    for ws in [int(v) for v in os.environ.get("IIR_CASES", "0,1,2,5").split(",")]:
         f = IIRFilter(ff, fb, IIRFilterType.SecondOrder, sample_dtype=np.float32, algo=sd.ALGO_FMA)
         sd.lib().sdsp_iir_set_tuning(f._h, 7, ws)
         variants[f"wscan{ws}"] = f
@@ -31,13 +34,18 @@ def main(rounds=8, log2n=30):
         torch.cuda.synchronize()
         outs[f"wscan{ws}"] = (o[: 1 << 22].cpu().numpy().astype(np.float64), o[-(1 << 20):].cpu().numpy().astype(np.float64))
         f.reset()
-    a = outs["wscan0"]
+    a = next(iter(outs.values()))
     agree = {k: max(float(np.linalg.norm(a[i] - b[i]) / np.linalg.norm(a[i])) for i in range(2))
              for k, b in outs.items()}
     d_out = torch.empty_like(d_in)
     times = {k: [] for k in variants}
+    keys = list(variants)
+    for _ in range(40):  # clocks settle
+        variants[keys[-1]].execute_block_device(d_in, n, d_out, s)
+    rng = np.random.default_rng(0)
     for _ in range(rounds):
-        for k, f in variants.items():
+        for k in rng.permutation(keys):
+            f = variants[k]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             f.execute_block_device(d_in, n, d_out, s)
