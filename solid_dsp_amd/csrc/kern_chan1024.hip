@@ -194,7 +194,15 @@ template <int S> __device__ __forceinline__ void row_swap(f2& a, f2& b) {
     b = f2{bx, by};
 }
 
-__device__ __forceinline__ void st_nt2(f2* p, f2 v) { __builtin_nontemporal_store(v, p); }
+#ifdef SDSP_CHAN_LAB
+__device__ int g_chan_plain_st;  // lab: plain instead of nontemporal output stores
+#endif
+__device__ __forceinline__ void st_nt2(f2* p, f2 v) {
+#ifdef SDSP_CHAN_LAB
+    if (g_chan_plain_st) { *p = v; return; }
+#endif
+    __builtin_nontemporal_store(v, p);
+}
 
 // one frame by one wave: buf holds v[p] at p; natural-order X to yf.  Packed
 // FP32 throughout (sdsp_pk.hpp: each complex add / multiply is one or two
@@ -502,7 +510,11 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 
 #ifdef SDSP_CHAN_LAB
 static int g_chan_lab = 0;
-extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) { g_chan_lab = v; }
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) {
+    g_chan_lab = v & 7;
+    const int plain = (v >> 3) & 1;  // bit 8: plain stores
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chan_plain_st), &plain, sizeof(int));
+}
 #endif
 
 // M = 1024, complex f32, K <= 8 taps per branch; false = not applicable

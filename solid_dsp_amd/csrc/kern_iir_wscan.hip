@@ -37,6 +37,13 @@ namespace sdsp {
 namespace {
 
 constexpr int kWsThreads = 256;
+
+#ifdef SDSP_IIR_LAB
+// ablations for tools/iir_ab.py (lab builds only, never in libsdsp.so): 1 no zero-state
+// run, 2 no scan, 4 no correction, 8 no HBM loads, 16 no HBM stores; variants:
+// 32 plain (not nontemporal) loads, 64 plain stores
+__device__ int g_iir_lab;
+#endif
 constexpr int kWsWaves = kWsThreads / 64;
 
 // chunk of CB bytes per lane (B = CB / sizeof(I) samples); LDS rows padded by
@@ -201,6 +208,11 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 #pragma unroll
     for (int d = 0; d < D; ++d) carry[d] = cin ? cin[((long long)ch * nwaves + gw) * D + d] : zero_v<I>();
     const bool agg = gagg != nullptr;  // aggregate pass: the wave's zero-carry end state only
+#ifdef SDSP_IIR_LAB
+    const int lab = __builtin_amdgcn_readfirstlane(g_iir_lab);
+#else
+    constexpr int lab = 0;
+#endif
 
     // interior tiles are read with straight-line 16-byte loads, one tile ahead of
     // the compute (a per-vector branch would serialise the HBM round trips)
@@ -211,7 +223,9 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         if (interior_at(k0)) {
 #pragma unroll
             for (int j = 0; j < kVecPerRow; ++j)
-                pre[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + k0) + lane + 64 * j);
+                pre[j] = (lab & 8)    ? v4u{(unsigned)lane, 0u, 0u, (unsigned)j}
+                         : (lab & 32) ? reinterpret_cast<const v4u*>(x + k0)[lane + 64 * j]
+                                      : __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + k0) + lane + 64 * j);
         }
     }
 
@@ -242,7 +256,9 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             if (t + 1 < tpw && interior_at(kn)) {
 #pragma unroll
                 for (int j = 0; j < kVecPerRow; ++j)
-                    pre[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + kn) + lane + 64 * j);
+                    pre[j] = (lab & 8)    ? v4u{(unsigned)lane, (unsigned)t, 0u, (unsigned)j}
+                             : (lab & 32) ? reinterpret_cast<const v4u*>(x + kn)[lane + 64 * j]
+                                          : __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + kn) + lane + 64 * j);
             }
         }
         wave_sync();
@@ -253,7 +269,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 #pragma unroll
             for (int d = 0; d < D; ++d) s[d] = zero_v<I>();
 #pragma unroll 2
-            for (int o = 0; o < kVecPerRow; ++o) {
+            for (int o = 0; o < kVecPerRow && !(lab & 1); ++o) {
                 I e[E];
                 const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
                 __builtin_memcpy(e, &val, 16);
@@ -267,7 +283,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             for (int d = 0; d < D; ++d) s[d] = st_in[d];
         }
         // 3. fold the carry into lane 0, then the inclusive scan over lanes
-        {
+        if (!(lab & 2)) {
             I a[D];
             sys_matvec<ND>(sP, carry, a);
             if (lane == 0) {
@@ -276,7 +292,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             }
         }
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = 0; k < 6 && !(lab & 2); ++k) {
             const int off = 1 << k;
             I prev[D], a[D];
 #pragma unroll
@@ -317,7 +333,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             }
         } else {
 #pragma unroll 2
-            for (int o = 0; o < kVecPerRow; ++o) {
+            for (int o = 0; o < kVecPerRow && !(lab & 4); ++o) {
                 I e[E];
                 const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
                 __builtin_memcpy(e, &val, 16);
@@ -361,7 +377,9 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             for (int j = 0; j < kVecPerRow; ++j) {
                 const int v = lane + 64 * j;
                 const v4u val = *reinterpret_cast<const v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16);
-                __builtin_nontemporal_store(val, reinterpret_cast<v4u*>(y + k0) + v);
+                if ((lab & 16) && val.x != 0x7fc01234u) continue;  // ablation: stores dropped
+                if (lab & 64) reinterpret_cast<v4u*>(y + k0)[v] = val;  // lab: plain store
+                else __builtin_nontemporal_store(val, reinterpret_cast<v4u*>(y + k0) + v);
             }
         } else {
             for (int j = 0; j < kVecPerRow; ++j) {
@@ -846,6 +864,12 @@ hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
 }
 
 }  // namespace
+
+#ifdef SDSP_IIR_LAB
+extern "C" __attribute__((visibility("default"))) int sdsp_lab_set_iir_ablation(int v) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_iir_lab), &v, sizeof(int));
+}
+#endif
 
 size_t iir_wscan_waves(int dtype, const IirArgs& a) {
     const int B = iir_wscan_chunk(dtype, a.ws_variant == 1 ? 1 : 0);
