@@ -196,6 +196,7 @@ template <int S> __device__ __forceinline__ void row_swap(f2& a, f2& b) {
 
 #ifdef SDSP_CHAN_LAB
 __device__ int g_chan_plain_st;  // lab: plain instead of nontemporal output stores
+__device__ int g_chan_nt_ld;     // lab: nontemporal input loads
 #endif
 __device__ __forceinline__ void st_nt2(f2* p, f2 v) {
 #ifdef SDSP_CHAN_LAB
@@ -314,11 +315,20 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
     auto branch = [&](int j) { return kPair ? 2 * t + j : t + kThreads * j; };
     auto load_pair = [&](const f2* xf, f2 (&v)[kNB]) {
         if constexpr (kPair) {
-            const pk::f4v q = *reinterpret_cast<const pk::f4v*>(xf + kM - 2 - 2 * t);
+            const pk::f4v* qp = reinterpret_cast<const pk::f4v*>(xf + kM - 2 - 2 * t);
+#ifdef SDSP_CHAN_LAB
+            const pk::f4v q = g_chan_nt_ld ? __builtin_nontemporal_load(qp) : *qp;
+#else
+            const pk::f4v q = *qp;
+#endif
             v[0] = f2{q.z, q.w};  // branch 2t:   x[M-1-2t]
             v[1] = f2{q.x, q.y};  // branch 2t+1: x[M-2-2t]
         } else {
+#ifdef SDSP_CHAN_LAB
+            v[0] = g_chan_nt_ld ? __builtin_nontemporal_load(xf + kM - 1 - t) : xf[kM - 1 - t];
+#else
             v[0] = xf[kM - 1 - t];
+#endif
         }
     };
     float c[kNB][K];
@@ -512,8 +522,9 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 static int g_chan_lab = 0;
 extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) {
     g_chan_lab = v & 7;
-    const int plain = (v >> 3) & 1;  // bit 8: plain stores
+    const int plain = (v >> 3) & 1, ntld = (v >> 4) & 1;  // bit 8: plain stores, bit 16: nontemporal loads
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chan_plain_st), &plain, sizeof(int));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chan_nt_ld), &ntld, sizeof(int));
 }
 #endif
 
