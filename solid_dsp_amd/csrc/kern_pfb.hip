@@ -7,10 +7,10 @@
 // (src/filter/fir/interp.rs:102-111) pushes each input and emits all M
 // branches, so
 //     out[j*M + p] = sum_{i<K} cb[p][i] * x[j-i]
-// Each lane owns one output; lanes of a wave cover consecutive (j, p) so the
-// stores are contiguous, the sample x[j-i] is a broadcast within the wave and
-// the M*K coefficients stay L1/L2 resident.  Summation order is the
-// reference's (EXACT) or fused.
+// Three kernels, same sums: interp_tile_kernel (M = 2^m, K in {4, 8, 16}, the
+// interpolator shape), pfb_stage_kernel (every other shape whose tile fits in
+// LDS) and pfb_kernel (one lane per output, the fallback for very long
+// branches).  Summation order is the reference's (EXACT) or fused.
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 
@@ -40,6 +40,54 @@ pfb_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* __restr
         I acc = zero_v<I>();
         for (int i = 0; i < K; ++i) acc = mac<EXACT>(acc, c[i], pfb_ext(x, hist, j - i, H));
         y[o] = acc;
+    }
+}
+
+// Staged form for every other shape: a 256-lane workgroup owns T consecutive
+// inputs of one channel (T M ~ 4096 outputs); the T + K - 1 samples they need
+// and (when they fit) the M K branch coefficients are staged once in LDS with
+// coalesced loads, then the lanes walk the tile's outputs in order (stores
+// contiguous across the workgroup), each the reference dot product
+// sum_{i<K} cb[p][i] x[j-i] in the reference order -- where pfb_kernel above
+// re-read K samples and K coefficients from global memory per output and
+// divided 64-bit indices.
+constexpr int kPfbStageBytes = 48 * 1024;
+
+template <typename C, typename I, bool EXACT, bool CB_LDS>
+__global__ void __launch_bounds__(256)
+pfb_stage_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* __restrict__ cb, I* __restrict__ y,
+                 long long n, int K, int M, int H, int T) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char pfb_lds[];
+    I* xs = reinterpret_cast<I*>(pfb_lds);  // xs[s] = x[j0 - K + 1 + s]
+    const int ch = blockIdx.y;
+    x += (long long)ch * n;
+    hist += (long long)ch * H;
+    y += (long long)ch * n * M;
+    const long long j0 = (long long)blockIdx.x * T;
+    const int nt = n - j0 < T ? (int)(n - j0) : T;
+    const int ns = nt + K - 1;
+    const C* cbs = cb;
+    if constexpr (CB_LDS) {
+        C* c = reinterpret_cast<C*>(pfb_lds + ((size_t)(T + K - 1) * sizeof(I) + 15) / 16 * 16);
+        for (int i = threadIdx.x; i < M * K; i += 256) c[i] = cb[i];
+        cbs = c;
+    }
+    const long long base = j0 - K + 1;
+    if (base >= 0) {
+        for (int i = threadIdx.x; i < ns; i += 256) xs[i] = x[base + i];
+    } else {
+        for (int i = threadIdx.x; i < ns; i += 256) xs[i] = pfb_ext(x, hist, base + i, H);
+    }
+    __syncthreads();
+    const unsigned um = (unsigned)M, total = (unsigned)nt * um;
+    I* yt = y + j0 * M;
+    for (unsigned o = threadIdx.x; o < total; o += 256) {
+        const unsigned j = o / um, p = o - j * um;
+        const C* c = cbs + (size_t)p * K;
+        const I* w = xs + j + K - 1;  // w[-i] = x[j0 + j - i]
+        I acc = zero_v<I>();
+        for (int i = 0; i < K; ++i) acc = mac<EXACT>(acc, c[i], w[-i]);
+        yt[o] = acc;
     }
 }
 
@@ -136,6 +184,27 @@ template <typename C, typename I>
 hipError_t launch_pfb_t(const PfbArgs& a, hipStream_t s) {
     if (interp_tile_applies<I>(a))
         return a.exact ? launch_interp_tile<C, I, true>(a, s) : launch_interp_tile<C, I, false>(a, s);
+#ifndef SDSP_PFB_LAB  // lab builds keep the per-output kernel for A/B (tools/lab.mk)
+    {
+        const int T = a.M >= 4096 ? 1 : 4096 / a.M;
+        const size_t xb = ((size_t)(T + a.K - 1) * sizeof(I) + 15) / 16 * 16, cbb = (size_t)a.M * a.K * sizeof(C);
+        if (xb <= kPfbStageBytes && (unsigned long long)T * a.M < (1ULL << 31)) {
+            const bool cb_lds = xb + cbb <= kPfbStageBytes;
+            const size_t lds = xb + (cb_lds ? cbb : 0);
+            dim3 g((unsigned)((a.n + T - 1) / T), (unsigned)a.channels);
+#define SDSP_PFB_STAGE(EX, CBL)                                                                                  \
+    hipLaunchKernelGGL((pfb_stage_kernel<C, I, EX, CBL>), g, dim3(256), lds, s, (const I*)a.x, (const I*)a.hist, \
+                       (const C*)a.cb, (I*)a.y, (long long)a.n, a.K, a.M, a.H, T)
+            if (a.exact) {
+                if (cb_lds) SDSP_PFB_STAGE(true, true); else SDSP_PFB_STAGE(true, false);
+            } else {
+                if (cb_lds) SDSP_PFB_STAGE(false, true); else SDSP_PFB_STAGE(false, false);
+            }
+#undef SDSP_PFB_STAGE
+            return hipGetLastError();
+        }
+    }
+#endif
     const long long total = (long long)a.n * a.M;
     long long blocks = (total + 255) / 256;
     if (blocks > 65536) blocks = 65536;

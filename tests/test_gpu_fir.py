@@ -482,3 +482,19 @@ def test_per_sample_execute_bit_parity(dt, cdt, sdt, L, M):
     ref += list(o.execute_block(x[230:]))
     assert len(got) == len(ref)
     assert bits_equal(np.array(got, dtype=sdt), np.array(ref, dtype=sdt))
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", DTYPES)
+@pytest.mark.parametrize("L,M,n1,n2", [(21, 3, 5000, 3333), (240, 24, 700, 9001), (3000, 1000, 9, 5),
+                                       (6000, 2, 4100, 77), (12000, 2, 300, 50)])
+def test_pfb_staged_kernel_bit_parity(dt, cdt, sdt, L, M, n1, n2):
+    """the LDS-staged generic kernel (tiles of ~4096 outputs, coefficients staged when
+    they fit) and, for the longest branches, the per-output fallback: bit-identical to
+    the restatement over two calls (tile edges, history), for every dtype"""
+    rng = np.random.default_rng(L + M + dt)
+    h = rand(rng, L, cdt)
+    x = rand(rng, n1 + n2, sdt)
+    p = PolyPhaseFilterBank(h, M, cdt(1.0), sample_dtype=sdt)
+    o = O.pfb(dt, h, M, cdt(1.0))
+    assert bits_equal(p.execute_block(x[:n1]), o.execute_block(x[:n1]))
+    assert bits_equal(p.execute_block(x[n1:]), o.execute_block(x[n1:]))

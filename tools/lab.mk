@@ -9,7 +9,7 @@ CSRC = solid_dsp_amd/csrc
 OBJ = solid_dsp_amd/_build/obj
 HIPFLAGS = --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result \
            -fvisibility=hidden -Iinclude -I$(CSRC)
-LAB_SRC = kern_fir_ols_os kern_chan1024 kern_iir_wscan
+LAB_SRC = kern_fir_ols_os kern_chan1024 kern_iir_wscan kern_pfb
 OUT = tools/_build/libsdsp_lab.so
 PRODUCT_OBJS = $(filter-out $(patsubst %,$(OBJ)/%.o,$(LAB_SRC)),$(wildcard $(OBJ)/*.o))
 
@@ -17,7 +17,7 @@ all: $(OUT)
 
 tools/_build/lab/%.o: $(CSRC)/%.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
 	@mkdir -p tools/_build/lab
-	$(HIPCC) $(HIPFLAGS) -DSDSP_OLS_LAB -DSDSP_CHAN_LAB -DSDSP_IIR_LAB -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DSDSP_OLS_LAB -DSDSP_CHAN_LAB -DSDSP_IIR_LAB -DSDSP_PFB_LAB -c $< -o $@
 
 $(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_SRC)) $(PRODUCT_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^
