@@ -17,6 +17,7 @@
 // the previous call), which is what makes the delay line persist across
 // execute_block calls exactly as the reference's Window does.
 #include "sdsp_device.hpp"
+#include <cstdlib>
 #include "sdsp_kernels.hpp"
 
 namespace sdsp {
@@ -138,6 +139,8 @@ fir_direct_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* 
 // Tap i = k*M + p.  LDS row rho holds the M samples ext(j_{m0} + (rho-K+1)*M - p),
 // p = 0..M-1, so lane u reads row u-k+K-1 left to right for tap group k — the
 // reference order — and lanes hit rows 16 bytes apart in bank space.
+constexpr int kStageU = 16;  // staging loads in flight per lane (32 or 40 measured slower)
+
 template <typename C, typename I, bool EXACT>
 __global__ void __launch_bounds__(kThreads)
 decim_direct_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* __restrict__ cr,
@@ -155,10 +158,33 @@ decim_direct_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C
     const long long jm0 = j0 + m0 * M;
     const int tid = threadIdx.x;
 
-    for (int f = tid; f < rows * M; f += blockDim.x) {
-        const int rho = f / M, p = f - rho * M;
-        const long long j = jm0 + (long long)(rho - K + 1) * M - p;
-        *reinterpret_cast<I*>(lds + rho * rowBytes + p * (int)sizeof(I)) = ext_load(x, hist, j, n, L - 1);
+    // stage: interior tiles read the contiguous inputs x[base + f] with kStageU loads in
+    // flight per lane (f -> row f / M, slot M-1 - f % M); edge tiles go through ext_load
+    const long long base = jm0 - (long long)(K - 1) * M - (M - 1);
+    const int total = rows * M;
+    if (base >= 0 && base + total <= n) {
+        for (int f0 = 0; f0 < total; f0 += kStageU * (int)blockDim.x) {
+            I v[kStageU];
+#pragma unroll
+            for (int u = 0; u < kStageU; ++u) {
+                const int f = f0 + u * (int)blockDim.x + tid;
+                if (f < total) v[u] = x[base + f];
+            }
+#pragma unroll
+            for (int u = 0; u < kStageU; ++u) {
+                const int f = f0 + u * (int)blockDim.x + tid;
+                if (f < total) {
+                    const int rho = f / M, q = f - rho * M;
+                    *reinterpret_cast<I*>(lds + rho * rowBytes + (M - 1 - q) * (int)sizeof(I)) = v[u];
+                }
+            }
+        }
+    } else {
+        for (int f = tid; f < total; f += blockDim.x) {
+            const int rho = f / M, p = f - rho * M;
+            const long long j = jm0 + (long long)(rho - K + 1) * M - p;
+            *reinterpret_cast<I*>(lds + rho * rowBytes + p * (int)sizeof(I)) = ext_load(x, hist, j, n, L - 1);
+        }
     }
     __syncthreads();
     const long long m = m0 + tid;
@@ -168,9 +194,13 @@ decim_direct_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C
         const I* row = reinterpret_cast<const I*>(lds + (tid - k + K - 1) * rowBytes);
         const C* ck = cr + k * M;
         const int pe = min(M, L - k * M);
+        // unrolled so that a run of LDS reads is in flight before the (ordered) sums
+        // consume it; the summation order is unchanged
         if (pe == M) {
+#pragma unroll 16
             for (int p = 0; p < M; ++p) acc = mac<EXACT>(acc, ck[p], row[p]);
         } else {
+#pragma unroll 16
             for (int p = 0; p < pe; ++p) acc = mac<EXACT>(acc, ck[p], row[p]);
         }
     }
@@ -234,8 +264,15 @@ hipError_t launch_decim_direct_t(const FirArgs& a, hipStream_t s) {
     const C scale = *reinterpret_cast<const C*>(a.scale);
     const int M = a.M, L = a.L, K = (L + M - 1) / M;
     const size_t rowBytes = (size_t)M * sizeof(I) + 16;
-    int T = kThreads;
-    while (T > 64 && (size_t)(T + K - 1) * rowBytes > 64 * 1024) T -= 64;
+    // outputs (= lanes) per workgroup: the largest multiple of 64 whose LDS rows fit
+    // in 40 KB, so that several workgroups per CU overlap their staging and sums
+    static const int tmax = [] {
+        const char* e = std::getenv("SDSP_DECIM_T");
+        return e ? std::atoi(e) : kThreads;
+    }();
+    int T = tmax;
+    while (T > 64 && (size_t)(T + K - 1) * rowBytes > 40 * 1024) T -= 64;
+    if ((size_t)(T + K - 1) * rowBytes > 64 * 1024) T = 64;
     const size_t lds = (size_t)(T + K - 1) * rowBytes;
     if (lds <= 64 * 1024) {
         dim3 grid((unsigned)((a.nout + T - 1) / T), (unsigned)a.channels);
