@@ -17,7 +17,6 @@
 // the previous call), which is what makes the delay line persist across
 // execute_block calls exactly as the reference's Window does.
 #include "sdsp_device.hpp"
-#include <cstdlib>
 #include "sdsp_kernels.hpp"
 
 namespace sdsp {
@@ -266,11 +265,7 @@ hipError_t launch_decim_direct_t(const FirArgs& a, hipStream_t s) {
     const size_t rowBytes = (size_t)M * sizeof(I) + 16;
     // outputs (= lanes) per workgroup: the largest multiple of 64 whose LDS rows fit
     // in 40 KB, so that several workgroups per CU overlap their staging and sums
-    static const int tmax = [] {
-        const char* e = std::getenv("SDSP_DECIM_T");
-        return e ? std::atoi(e) : kThreads;
-    }();
-    int T = tmax;
+    int T = kThreads;
     while (T > 64 && (size_t)(T + K - 1) * rowBytes > 40 * 1024) T -= 64;
     if ((size_t)(T + K - 1) * rowBytes > 64 * 1024) T = 64;
     const size_t lds = (size_t)(T + K - 1) * rowBytes;
