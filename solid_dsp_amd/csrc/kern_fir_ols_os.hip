@@ -74,17 +74,52 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
     return pmul(d[a - 1], c[b - 1]);
 }
 
+#ifdef SDSP_OLS_LAB
+// per-CU count of workgroups whose segment loads are in flight (lab bits 8/16/24)
+__device__ unsigned int g_ols_cu_loading[8 * 256];
+
+__device__ __forceinline__ unsigned int* cu_slot() {
+    unsigned int xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    return g_ols_cu_loading + ((xcc & 7) << 8) + ((hw >> 8) & 255);
+}
+#endif
+
 }  // namespace
 
 // VAR = 0 is the product kernel; tools/lab.mk builds other values (SDSP_OLS_LAB)
 // for in-process A/B runs -- they are never part of libsdsp.so.  Lab bits:
 // 1 block barriers at the wave-local phase boundaries; 2 no HBM traffic
-// (ablation: outputs dropped); 4 HBM traffic only (ablation: no transform).
+// (ablation: outputs dropped); 4 HBM traffic only (ablation: no transform);
+// 8/16/24: at most 1/2/3 workgroups per CU with segment loads in flight (a
+// per-CU ticket taken with vector atomics before the loads, returned once P1
+// has consumed them); 32: high wave priority while issuing loads and stores.
 template <int VAR>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
                                                int h2, f2* img, int t) {
     const int hi4 = t >> 4, lo4 = t & 15;
+#ifdef SDSP_OLS_LAB
+    constexpr unsigned kLim = (VAR >> 3) & 3;
+    unsigned int* slot = nullptr;
+    bool held = false;  // lane 0 of wave 0 holds a ticket (bounded wait: a lab run can never hang on it)
+    if constexpr (kLim != 0) {
+        slot = cu_slot();
+        if (t == 0) {
+            for (int tries = 0; tries < 4096; ++tries) {
+                if (__hip_atomic_fetch_add(slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < kLim) {
+                    held = true;
+                    break;
+                }
+                __hip_atomic_fetch_add(slot, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_s_sleep(4);
+            }
+        }
+        __syncthreads();
+    }
+    if constexpr (VAR & 32) __builtin_amdgcn_s_setprio(3);
+#endif
     const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, 32768, kBufWord3);
     const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, 32768, kBufWord3);
     const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
@@ -95,10 +130,19 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         if constexpr (VAR & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
         else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
     }
+#ifdef SDSP_OLS_LAB
+    if constexpr (VAR & 32) __builtin_amdgcn_s_setprio(0);
+#endif
     if constexpr (VAR & 4) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
             if (r >= h2) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[r]), ry, 8 * t, 2048 * r, 0);
+#ifdef SDSP_OLS_LAB
+        if constexpr (kLim != 0) {
+            __syncthreads();
+            if (held) __hip_atomic_fetch_add(slot, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#endif
         return;
     }
     // twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build)
@@ -119,6 +163,11 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
 #pragma unroll
     for (int k = 0; k < 16; ++k) col[k * kRow] = k == 0 ? v[0] : pmul(v[kout(k)], tw_pair(Cb, Da, k));
     __syncthreads();
+#ifdef SDSP_OLS_LAB
+    if constexpr (kLim != 0) {
+        if (held) __hip_atomic_fetch_add(slot, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
 
     // P2: lane (k0 = hi4, n0 = lo4): DFT16 n1 -> k1, * W256^(n0 k1) -> (k0, 16 k1 + n0)
     f2* r2 = img + hi4 * kRow + lo4;  // (hi4, 16 j + lo4) at r2[17 j]
@@ -175,6 +224,9 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         if (acc.x == 1.2345e30f) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc), ry, 8 * t, 0, 0);
         return;
     }
+#ifdef SDSP_OLS_LAB
+    if constexpr (VAR & 32) __builtin_amdgcn_s_setprio(3);
+#endif
 #pragma unroll
     for (int r = 0; r < 16; ++r)
         if (r >= h2) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, 0);
@@ -194,9 +246,12 @@ fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const
 }
 
 #ifdef SDSP_OLS_LAB
-static int g_lab_variant = 0;
-extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int, int) { g_lab_variant = v; }
-#define SDSP_LAB_VARIANTS(X) X(1) X(2) X(3) X(4)
+static int g_lab_variant = 0, g_lab_lds = 0;
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int lds, int) {
+    g_lab_variant = v;
+    g_lab_lds = lds;
+}
+#define SDSP_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(8) X(16) X(24) X(12) X(20) X(28) X(32) X(36) X(48)
 #endif
 
 hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
@@ -208,7 +263,8 @@ hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n,
 #ifdef SDSP_OLS_LAB
 #define SDSP_LAB_CASE(V)                                                                                       \
     if (g_lab_variant == V) {                                                                                  \
-        hipLaunchKernelGGL(fir_ols_os_kernel<V>, grid, dim3(256), 0, s, (const f2*)x, (const float4*)p.d_pkt,  \
+        hipLaunchKernelGGL(fir_ols_os_kernel<V>, grid, dim3(256), g_lab_lds, s, (const f2*)x,                  \
+                           (const float4*)p.d_pkt,                                                             \
                            (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows);            \
         return hipGetLastError();                                                                              \
     }

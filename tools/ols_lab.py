@@ -48,7 +48,12 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
             continue
         L.sdsp_lab_set_ols_variant(*v)
         f.reset()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
         f.execute_block_device(d_in, n, d_out, s)
+        e1.record(s)
+        torch.cuda.synchronize()
+        print("first run var%d:%d:%d %.3f ms" % (v + (e0.elapsed_time(e1),)), flush=True)
         outs[v] = np.concatenate([d_out[: 1 << 22].cpu().numpy(), d_out[-(1 << 20):].cpu().numpy()])
     ref = outs.get((0, 0, 1))
     for v, o in outs.items():
@@ -60,7 +65,8 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
     rng = np.random.default_rng(1)
     times = {v: [] for v in variants}
     order = list(variants)
-    for _ in range(rounds):
+    for i in range(rounds):
+        print("round", i, flush=True)
         rng.shuffle(order)
         for v in order:
             L.sdsp_lab_set_ols_variant(*v)
