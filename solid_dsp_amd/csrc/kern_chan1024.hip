@@ -290,6 +290,10 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
 #ifdef SDSP_CHAN_LAB
     const int lab = xcd >> 4;  // ablations (tools/chan_ab.py): 1 no FFT, 2 no loads, 4 no stores
     xcd &= 1;
+    if ((lab & 24) && ((bid >> 3) & 1)) {  // stagger: desynchronise the rounds of neighbouring workgroups
+        const int ns = ((lab & 8) ? 2 : 0) + ((lab & 16) ? 1 : 0);
+        for (int i = 0; i < ns; ++i) __builtin_amdgcn_s_sleep(127);
+    }
 #else
     constexpr int lab = 0;
 #endif
@@ -521,7 +525,7 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 #ifdef SDSP_CHAN_LAB
 static int g_chan_lab = 0;
 extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) {
-    g_chan_lab = v & 7;
+    g_chan_lab = (v & 7) | ((v >> 2) & 24);  // bits 32 / 64: odd workgroups start ~6.8 / ~3.4 us late
     const int plain = (v >> 3) & 1, ntld = (v >> 4) & 1;  // bit 8: plain stores, bit 16: nontemporal loads
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chan_plain_st), &plain, sizeof(int));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chan_nt_ld), &ntld, sizeof(int));

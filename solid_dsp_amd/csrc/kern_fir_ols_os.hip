@@ -132,6 +132,14 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     }
 #ifdef SDSP_OLS_LAB
     if constexpr (VAR & 32) __builtin_amdgcn_s_setprio(0);
+    if constexpr (kLim != 0 && (VAR & 64)) {  // ticket back as soon as the loads have landed
+#pragma unroll
+        for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(v[r]));
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        __syncthreads();
+        if (held) __hip_atomic_fetch_add(slot, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        held = false;
+    }
 #endif
     if constexpr (VAR & 4) {
 #pragma unroll
@@ -251,7 +259,20 @@ extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(
     g_lab_variant = v;
     g_lab_lds = lds;
 }
-#define SDSP_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(8) X(16) X(24) X(12) X(20) X(28) X(32) X(36) X(48)
+__global__ void ols_hwid_probe_kernel(unsigned int* out) {
+    unsigned int xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (threadIdx.x == 0) {
+        out[2 * blockIdx.x] = xcc;
+        out[2 * blockIdx.x + 1] = hw;
+    }
+}
+extern "C" __attribute__((visibility("default"))) int sdsp_lab_hwid_probe(unsigned int* d_out, int blocks) {
+    hipLaunchKernelGGL(ols_hwid_probe_kernel, dim3(blocks), dim3(64), 40000, 0, d_out);
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
+#define SDSP_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(8) X(16) X(24) X(12) X(20) X(28) X(32) X(36) X(48) X(80) X(88) X(84) X(92)
 #endif
 
 hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,

@@ -196,9 +196,18 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         return k % Mi == 0 ? x[k / Mi] : zero_v<I>();
     };
 
-    const long long gw = (long long)blockIdx.x * kWsWaves + wave;  // wave's segment
-    const long long segc = (long long)tpw * 64 - wc;                  // chunks per segment
-    const long long c_lo = gw * segc;                                 // first chunk of the segment
+#ifdef SDSP_IIR_LAB
+    const int lab = __builtin_amdgcn_readfirstlane(g_iir_lab);
+#else
+    constexpr int lab = 0;
+#endif
+    // XCD-ordered blocks (gridDim.x is a multiple of 8): block b runs on XCD b % 8 and
+    // takes the (b / 8)-th block of that XCD's contiguous eighth, so each XCD streams
+    // one window of neighbouring segments (cfg3: -1.6 %, the HBM-only pattern -2 %)
+    const long long bx = (long long)(blockIdx.x & 7) * (gridDim.x / 8) + (blockIdx.x >> 3);
+    const long long gw = bx * kWsWaves + wave;        // wave's segment
+    const long long segc = (long long)tpw * 64 - wc;  // chunks per segment
+    const long long c_lo = gw * segc;                 // first chunk of the segment
     const long long k_lo = c_lo * B;
     if (k_lo >= nd) return;
 
@@ -208,11 +217,6 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 #pragma unroll
     for (int d = 0; d < D; ++d) carry[d] = cin ? cin[((long long)ch * nwaves + gw) * D + d] : zero_v<I>();
     const bool agg = gagg != nullptr;  // aggregate pass: the wave's zero-carry end state only
-#ifdef SDSP_IIR_LAB
-    const int lab = __builtin_amdgcn_readfirstlane(g_iir_lab);
-#else
-    constexpr int lab = 0;
-#endif
 
     // interior tiles are read with straight-line 16-byte loads, one tile ahead of
     // the compute (a per-vector branch would serialise the HBM round trips)
@@ -780,6 +784,10 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+#ifdef SDSP_IIR_LAB
+static int g_iir_lab_host = 0;
+#endif
+
 template <int CB> int wscan_tpw(long long nch) {
     // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
     int tpw = (int)(nch / (64LL * 4096));
@@ -792,12 +800,16 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     constexpr int D = ND ? ND : 2 * S;
     const long long nd = (long long)a.n * a.Mi;  // domain samples
     const long long nch = (nd + B - 1) / B;
-    const int tpw = wscan_tpw<CB>(nch);
+    int tpw = wscan_tpw<CB>(nch);
+#ifdef SDSP_IIR_LAB
+    if (a.wc > 0 && ((g_iir_lab_host >> 8) & 15)) tpw = (g_iir_lab_host >> 8) & 15;  // lab: tiles per wave
+#endif
     const long long segc = (long long)tpw * 64 - a.wc;
     const long long waves = (nch + segc - 1) / segc;
     const bool exact = a.wc == 0;  // exact inter-wave carries: aggregate pass + carry scan first
     if (exact && (!a.Phi || !a.G || !a.Cin || (size_t)waves > a.scratch_waves)) return hipErrorInvalidValue;
-    dim3 grid((unsigned)((waves + kWsWaves - 1) / kWsWaves), (unsigned)a.channels);
+    // whole eighths for the XCD-ordered block map (surplus blocks find no segment and return)
+    dim3 grid((unsigned)((waves + 8 * kWsWaves - 1) / (8 * kWsWaves) * 8), (unsigned)a.channels);
     // 16-byte vector path: aligned bases and channel strides
     const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
                         (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
@@ -867,6 +879,7 @@ hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
 
 #ifdef SDSP_IIR_LAB
 extern "C" __attribute__((visibility("default"))) int sdsp_lab_set_iir_ablation(int v) {
+    g_iir_lab_host = v;  // bits 8-11: tiles per wave (warm-up scans)
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_iir_lab), &v, sizeof(int));
 }
 #endif

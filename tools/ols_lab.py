@@ -31,6 +31,14 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
     from solid_dsp_amd.filter import firdes
     L = sd.lib()
     L.sdsp_lab_set_ols_variant.argtypes = [C.c_int, C.c_int, C.c_int]
+    if os.environ.get("OLS_HWID"):  # which CU slots the lab tickets use: distinct (XCC_ID, HW_ID[15:8])
+        nb = 4096
+        hb = torch.zeros(2 * nb, dtype=torch.int32, device="cuda")
+        assert L.sdsp_lab_hwid_probe(C.c_void_p(hb.data_ptr()), nb) == 0
+        a = hb.cpu().numpy().astype(np.int64).reshape(-1, 2)
+        keys = set(((a[:, 0] & 7) << 8 | ((a[:, 1] >> 8) & 255)).tolist())
+        print("hwid: %d distinct slots over %d blocks; xcc values %s; hw_id samples %s" % (
+            len(keys), nb, sorted(set(a[:, 0].tolist()))[:16], [hex(v) for v in a[:8, 1]]), flush=True)
     n = 1 << log2n
     h = firdes.firdes_kaiser(256, 0.1, 80.0, 0.0).astype(np.float32)
     d_in = torch.empty(n, dtype=torch.complex64, device="cuda")
