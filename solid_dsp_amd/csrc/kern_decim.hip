@@ -180,7 +180,7 @@ decim_poly_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* 
     y += (long long)ch * nout;
     hist += (long long)ch * (L - 1);
 
-    const long long wave_id = (long long)blockIdx.x * kPolyWaves + wave;
+    const long long wave_id = (long long)xcd_order(blockIdx.x, gridDim.x) * kPolyWaves + wave;  // XCD-ordered
     const long long gid = wave_id * G + g;
     const long long m_begin = gid * seg;
     if (m_begin >= nout) return;

@@ -48,13 +48,6 @@ __host__ __device__ constexpr int pad8(int s) { return s + (s >> 3); }
 
 template <typename T> __device__ inline cpx<T> conj_(cpx<T> a) { return {a.re, -a.im}; }
 
-// Workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 share one);
-// remap so each XCD streams its own contiguous eighth of the buffer — the
-// one-shot order that ran at copy speed in tools/pattern_probe.hip (ORD 2).
-__device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned nb) {
-    const unsigned q = nb / 8;
-    return b < 8 * q ? (b % 8) * q + b / 8 : b;
-}
 
 template <typename T>
 __device__ inline cpx<T> ext_at(const cpx<T>* __restrict__ x, const cpx<T>* __restrict__ hist, long long j, int H) {

@@ -64,4 +64,13 @@ __device__ inline O mac(O acc, C c, I s) {
 // Out type of Coef * In
 template <typename C, typename I> struct out_of { using type = I; };
 
+// Workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8 share one);
+// remap so each XCD streams its own contiguous eighth of the workgroups' data --
+// the one-shot order that ran at copy speed in tools/pattern_probe.hip (ORD 2).
+// A bijection on [0, nb): blocks past the last whole eighth keep their index.
+__device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned nb) {
+    const unsigned q = nb / 8;
+    return b < 8 * q ? (b % 8) * q + b / 8 : b;
+}
+
 }  // namespace sdsp
