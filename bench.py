@@ -67,9 +67,10 @@ def parse():
 
 
 def load_traffic(config, log2n, algo, kernel=""):
-    """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (profiles/*/pmc_summary_cfg*.json written by tools/pmc_summary.py), or None.
-    The summary must name the kernel this run launches (first word of `kernel`)."""
+    """(HBM bytes per launch of the dominant kernel, the summary file it came from)
+    from the committed PMC pass (profiles/*/pmc_summary_cfg*.json written by
+    tools/pmc_summary.py), or (None, None).  The summary must name the kernel this
+    run launches (first word of `kernel`)."""
     import glob
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"pmc_summary_cfg{config}.json")), reverse=True):
         try:
@@ -77,10 +78,10 @@ def load_traffic(config, log2n, algo, kernel=""):
                 d = json.load(f)
             if (d.get("log2n") == log2n and d.get("algo", algo) == algo
                     and d.get("kernel", "") and kernel.split()[0].startswith(d["kernel"])):
-                return d["hbm_bytes_per_launch"]
+                return d["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
         except (OSError, ValueError, KeyError):
             pass
-    return None
+    return None, None
 
 
 def stream_copy_gbps(torch, sd, nbytes=4 << 30, seconds=0.3):
@@ -1028,6 +1029,7 @@ def main():
         parity_ok = parity is None or parity <= tol
         if gather and gather["check"] is not None:
             parity_ok = parity_ok and gather["check"] <= tol
+        traffic, traffic_src = load_traffic(args.config, args.log2n, w.algo_name, w.kernel)
         out = {
             "metric": w.metric,
             "value": round(value, 1),
@@ -1045,7 +1047,7 @@ def main():
                        "kernel": w.kernel, "parallelism": f"channels sharded, independent per GPU x {world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": load_traffic(args.config, args.log2n, w.algo_name, w.kernel),
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_ms": round(kern_ms, 4), "kernel_ms_median": round(float(np.median(ev_ms)), 4),
                          "kernel_ms_min": round(float(np.min(ev_ms)), 4),
                          "algorithmic_bytes_per_launch": w.bytes_per_step,
