@@ -498,3 +498,17 @@ def test_pfb_staged_kernel_bit_parity(dt, cdt, sdt, L, M, n1, n2):
     o = O.pfb(dt, h, M, cdt(1.0))
     assert bits_equal(p.execute_block(x[:n1]), o.execute_block(x[:n1]))
     assert bits_equal(p.execute_block(x[n1:]), o.execute_block(x[n1:]))
+
+
+def test_default_handle_is_exact_on_large_blocks():
+    """A handle built without an algo runs the reference-order kernel at every block
+    size: a crcf block above the 65536-sample size where AUTO would pick overlap-save
+    is bit-identical to the f32 restatement (default paths never change results)."""
+    rng = np.random.default_rng(65537)
+    h = rng.standard_normal(256).astype(F32)
+    x = rand(rng, 70000, C64)
+    f = FIRFilter(h, F32(0.2), sample_dtype=C64)
+    o = O.fir(O.RC32, h, F32(0.2))
+    assert bits_equal(f.execute_block(x), o.execute_block(x))
+    d = DecimatingFIRFilter(h, F32(0.2), 32, sample_dtype=C64)
+    assert bits_equal(d.execute_block(x), O.decim(O.RC32, h, F32(0.2), 32).execute_block(x))

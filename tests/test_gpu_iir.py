@@ -444,3 +444,15 @@ def test_iir_rejects_in_place_and_orders_side_stream_state():
     assert bits_equal(to_host(out), r) and bits_equal(st, rst)
     tail = x[:5000]
     assert bits_equal(g.execute_block(tail), ref.execute_block(tail))
+
+
+def test_default_handle_is_exact_on_large_blocks():
+    """An IIR handle built without an algo keeps the reference-order recurrence on a
+    block above the 8192-sample size where AUTO would pick a scan: bit-identical to
+    the f32 restatement."""
+    ff, fb = (c.astype(np.float32) for c in butter())
+    rng = np.random.default_rng(8193)
+    x = rng.standard_normal(20000).astype(np.float32)
+    f = IIRFilter(ff, fb, SO, sample_dtype=np.float32)
+    o = O.iir(O.RR32, ff, fb, O.SECOND_ORDER)
+    assert bits_equal(f.execute_block(x), o.execute_block(x))
