@@ -183,19 +183,21 @@ class Cfg2FIR:
             worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
         return worst
 
-    def check_gathered(self, big, rng, width=4096):
-        """every rank's gathered output (channel = rank): two random windows each,
-        recomputed in f64 from that channel's synthetic inputs"""
+    @staticmethod
+    def expected(h, r, s, width):
+        """outputs [s, s + width) of channel r, recomputed by the f64 restatement from the
+        channel's synthetic inputs (parallel.fir_input_window)"""
         import oracle_lib as O
-        worst, L = 0.0, self.taps
-        for r in range(big.shape[0]):
-            for _ in range(2):
-                s = int(rng.integers(L, self.n - width))
-                xs = O.synth(SEED, r, s - (L - 1), width + L - 1, complex_=True).astype(np.complex128)
-                ref = O.fir(O.RC64, self.h.astype(np.float64), 0.2).execute_block(xs)[L - 1:]
-                ys = big[r, s: s + width].cpu().numpy()
-                worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
-        return worst
+        from solid_dsp_amd import parallel as P
+        first, count, drop = P.fir_input_window(s, width, len(h))
+        xs = O.synth(SEED, r, first, count, complex_=True).astype(np.complex128)
+        return O.fir(O.RC64, np.asarray(h, np.float64), 0.2).execute_block(xs)[drop:]
+
+    def check_gathered(self, big, rng, width=4096):
+        """every rank's gathered output (channel = rank): two random windows each"""
+        from solid_dsp_amd import parallel as P
+        return P.check_gathered(big, lambda r, s, w: Cfg2FIR.expected(self.h, r, s, w), rng, width, self.taps,
+                                self.n)
 
     def cpu(self, samples):
         import oracle_lib as O
@@ -303,19 +305,22 @@ class Cfg4Decim:
     def output(self):
         return self.d_out[: self.n // 32]
 
-    def check_gathered(self, big, rng, width=4096):
-        """every rank's gathered decimated output (channel = rank), two random windows each"""
+    @staticmethod
+    def expected(h, r, m, width):
+        """decimated outputs [m, m + width) of channel r in f64 from the definition
+        y[m] = scale sum_j h[j] x[32 m + 31 - 255 + j] (parallel.decim_input_window)"""
         from numpy.lib.stride_tricks import sliding_window_view
         import oracle_lib as O
-        h, worst = self.h.astype(np.float64), 0.0
-        for r in range(big.shape[0]):
-            for _ in range(2):
-                m = int(rng.integers(8, self.n // 32 - width))
-                xs = O.synth(SEED, r, 32 * m - 224, 32 * width + 224, complex_=True).astype(np.complex128)
-                ref = sliding_window_view(xs, 256)[::32][:width] @ h / 32.0
-                ys = big[r, m: m + width].cpu().numpy()
-                worst = max(worst, float(np.linalg.norm(ys - ref) / np.linalg.norm(ref)))
-        return worst
+        from solid_dsp_amd import parallel as P
+        first, count = P.decim_input_window(m, width, len(h), 32)
+        xs = O.synth(SEED, r, first, count, complex_=True).astype(np.complex128)
+        return sliding_window_view(xs, len(h))[::32][:width] @ np.asarray(h, np.float64) / 32.0
+
+    def check_gathered(self, big, rng, width=4096):
+        """every rank's gathered decimated output (channel = rank), two random windows each"""
+        from solid_dsp_amd import parallel as P
+        return P.check_gathered(big, lambda r, m, w: Cfg4Decim.expected(self.h, r, m, w), rng, width, 8,
+                                self.n // 32)
 
     def cpu(self, samples):
         import oracle_lib as O
@@ -763,14 +768,29 @@ def dropin_costs(torch, sd, h32):
         g.execute(0.5 + 0.25j)
     dt = (time.perf_counter() - t0) / k
     out["per_sample_execute"] = {"us_per_call": round(dt * 1e6, 2), "calls": k,
-                                 "note": "FIRFilter<f64, Complex<f64>>::execute via the Python binding (ctypes adds ~1-2 us)"}
+                                 "note": "FIRFilter<f64, Complex<f64>>::execute via the Python binding (ctypes adds "
+                                         "~1 us): the host step against the handle's delay line"}
+    # the same calls from a compiled caller (what the Rust shim pays): solid_dsp_amd/csrc/step_bench.c,
+    # run as a child process (it opens its own device context)
+    import subprocess
+    exe = os.path.join(REPO, "solid_dsp_amd", "_build", "step_bench")
+    try:
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+        out["per_sample_c_abi"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+            {"error": (r.stderr or r.stdout)[-300:]}
+        out["per_sample_c_abi"]["note"] = ("C caller: execute / push with the host step (default) and with a "
+                                           "device launch per call (SDSP_TUNE_HOST_STEP = 0); the reference's "
+                                           "CPU loop takes ~0.36 us per sample (SURVEY §3.1)")
+    except (OSError, subprocess.TimeoutExpired, ValueError, IndexError) as e:
+        out["per_sample_c_abi"] = {"error": str(e)[-300:]}
     one = np.array([0.5 + 0.25j])
     t0 = time.perf_counter()
     for _ in range(k):
         g.execute_block(one)
     dt = (time.perf_counter() - t0) / k
     out["per_sample_execute_block_n1"] = {"us_per_call": round(dt * 1e6, 2), "calls": k,
-                                          "note": "execute_block with one sample: H2D + kernel + history + D2H + sync"}
+                                          "note": "execute_block with one sample (a host block: below the "
+                                                  "host-step threshold)"}
     return out
 
 
@@ -917,31 +937,46 @@ def spawn_ranks(n):
 
 
 def dry_run(args, rank, world):
-    """CPU-only rehearsal of the N-rank harness over gloo (no GPU, no oracle):
-    every rank filters its own channel (numpy), the job time is the max over
-    ranks, and the whole output of every rank is gathered on rank 0 in small
-    chunks and checked there against a recomputation."""
+    """CPU-only rehearsal of the N-rank harness over gloo (no GPU): every rank runs
+    its own channel (channel = rank) of the chosen workload's math -- config 2 the
+    cfg2 FIR, config 4 the cfg4 decimator, both on the f64 restatement standing in
+    for the device, stored as c32 like the device output -- the job time is the max
+    over ranks, the whole output of every rank is gathered on rank 0 in small chunks
+    (parallel.gather_full_to_root, the function the RCCL path calls) and checked there
+    by the same check_gathered the GPU run uses.  SDSP_DRYRUN_FAULT=shift makes the
+    last rank deliver its output one sample late (the check must then fail)."""
     import torch
     import torch.distributed as dist
+    import oracle_lib as O
     from solid_dsp_amd import parallel as P
     if world > 1:
         dist.init_process_group("gloo")
-    n, h = 1 << 14, np.hanning(64)
-
-    def channel(c):
-        x = np.random.default_rng([SEED, c]).standard_normal(2 * n).view(np.complex128)
-        return 0.2 * np.convolve(x, h)[:n]
+    cfg = args.config if args.config in (2, 4) else 2
+    n = 1 << 15
+    if cfg == 2:
+        h = O.firdes_kaiser(256, 0.1, 80.0, 0.0).astype(np.float32)
+        run = lambda x: O.fir(O.RC64, h.astype(np.float64), 0.2).execute_block(x)
+        expected = lambda r, s, w: Cfg2FIR.expected(h, r, s, w)
+        lo, hi, width = 256, n, 2048
+    else:
+        h = O.firdes_kaiser(256, 1.0 / 64, 80.0, 0.0).astype(np.float32)
+        run = lambda x: O.decim(O.RC64, h.astype(np.float64), 1.0 / 32, 32).execute_block(x)
+        expected = lambda r, m, w: Cfg4Decim.expected(h, r, m, w)
+        lo, hi, width = 8, n // 32, 256
     t0 = time.perf_counter()
-    y = channel(rank)
+    y = run(O.synth(SEED, rank, 0, n, complex_=True).astype(np.complex128)).astype(np.complex64)
+    if os.environ.get("SDSP_DRYRUN_FAULT") == "shift" and rank == world - 1:
+        y = np.concatenate([np.zeros(1, np.complex64), y[:-1]])
     wall = P.max_over_ranks(time.perf_counter() - t0)
     ranks = P.gather_to_root(torch.tensor([rank], dtype=torch.int64), 0)
-    big = P.gather_full_to_root(torch.from_numpy(y.view(np.float64).copy()), 0, chunk_bytes=1 << 15)
+    big = P.gather_full_to_root(torch.from_numpy(y), 0, chunk_bytes=1 << 14)
     if rank == 0:
-        ok = all(np.array_equal(big[r].numpy().view(np.complex128), channel(r)) for r in range(world))
-        print(json.dumps({"metric": "dry-run: rank launch + max-over-ranks timing + full gather (gloo, CPU)",
-                          "value": world * n / wall / 1e6, "unit": "Msamples/sec", "n_gpus": world,
-                          "ranks": [int(t.item()) for t in ranks], "gather_rows": int(big.shape[0]),
-                          "gather_ok": bool(ok), "dry_run": True}), flush=True)
+        worst = P.check_gathered(big, expected, np.random.default_rng(2), width, lo, hi)
+        print(json.dumps({"metric": "dry-run: rank launch + max-over-ranks timing + full gather + gathered-output "
+                          "check (gloo, CPU)", "value": world * n / wall / 1e6, "unit": "Msamples/sec",
+                          "n_gpus": world, "config": cfg, "ranks": [int(t.item()) for t in ranks],
+                          "gather_rows": int(big.shape[0]), "gather_check": worst,
+                          "gather_ok": bool(worst <= 1e-6), "dry_run": True}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -142,8 +142,14 @@ typedef enum {
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
     SDSP_TUNE_OLS_KERNEL = 14,   /* overlap-save interior segments (16-byte aligned rows): 0 (default) one-shot
                                     XCD-ordered kernel, 1 persistent packed kernel (L <= 1025), 2 scalar kernel */
-    SDSP_TUNE_CHAN_XCD_ORDER = 15 /* streaming channeliser: 1 (default) = each XCD walks a contiguous
+    SDSP_TUNE_CHAN_XCD_ORDER = 15, /* streaming channeliser: 1 (default) = each XCD walks a contiguous
                                      eighth of the frame chunks, 0 = launch order */
+    SDSP_TUNE_HOST_STEP = 16,     /* FIR / decimator: 1 (default) = execute(sample), push and host blocks with
+                                     n * len <= SDSP_TUNE_HOST_BLOCK_MACS run on the host against the
+                                     handle's delay line (single-channel handles, not the FFT algorithm;
+                                     reference arithmetic, bit-identical to the EXACT/FMA kernels);
+                                     0 = every call launches device work (one-sample step kernel) */
+    SDSP_TUNE_HOST_BLOCK_MACS = 17 /* host-block threshold in multiply-adds (default 65536) */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */

@@ -5,6 +5,7 @@ use crate::filter::{Filter, SdspPair};
 use crate::{check, device, sys};
 
 use std::error::Error;
+use std::fmt;
 use std::marker::PhantomData;
 
 use num::{Complex, Zero};
@@ -48,6 +49,19 @@ where
     }
     pub fn interpolation(&self) -> usize {
         self.interpolation
+    }
+}
+
+impl<Coef, In> Clone for InterpolatingFIRFilter<Coef, In> {
+    /// derive(Clone) (interp.rs:6): the filterbank with its window
+    fn clone(&self) -> Self {
+        InterpolatingFIRFilter { filterbank: self.filterbank.clone(), interpolation: self.interpolation }
+    }
+}
+
+impl<Coef, In> fmt::Debug for InterpolatingFIRFilter<Coef, In> {
+    fn fmt(&self, f: &mut fmt::Formatter) -> fmt::Result {
+        write!(f, "InterpolatingFIRFilter {{ interpolation: {} }}", self.interpolation)
     }
 }
 

@@ -4,6 +4,7 @@ use crate::filter::SdspPair;
 use crate::{check, device, sys};
 
 use std::error::Error;
+use std::fmt;
 use std::marker::PhantomData;
 
 use num::Zero;
@@ -78,6 +79,12 @@ impl<Coef, In> Clone for PolyPhaseFilterBank<Coef, In> {
         let mut h = std::ptr::null_mut();
         check(unsafe { sys::sdsp_pfb_clone(self.h, &mut h) });
         PolyPhaseFilterBank { h, _t: PhantomData }
+    }
+}
+
+impl<Coef, In> fmt::Debug for PolyPhaseFilterBank<Coef, In> {
+    fn fmt(&self, f: &mut fmt::Formatter) -> fmt::Result {
+        write!(f, "PolyPhaseFilterBank {{ filters: {} }}", unsafe { sys::sdsp_pfb_len(self.h) })
     }
 }
 

@@ -1,7 +1,9 @@
 //! `solid::filter` (src/filter/mod.rs:1-22): the `Filter` trait, unchanged, and the
 //! device-backed filter types.
 pub mod fir;
+pub mod firdes;
 pub mod iir;
+pub mod iirdes;
 
 use num::Complex;
 
@@ -21,6 +23,14 @@ pub trait Filter<I, O> {
 pub trait SdspPair: private::Sealed {
     const DTYPE: std::os::raw::c_int;
 }
+/// The pairs of the IIR family: real coefficients (the reference's `Conj + Real` bounds,
+/// src/filter/iir/mod.rs:244-262) over real or complex samples.
+pub trait SdspIirPair: SdspPair {
+    type Coef;
+    /// one coefficient the library reports in f64, in the Coef type (exact for f32: the
+    /// library divides f32 values in f64, and one rounding to f32 equals the f32 division)
+    fn coef_from_f64(v: f64) -> Self::Coef;
+}
 mod private {
     pub trait Sealed {}
 }
@@ -38,3 +48,18 @@ pair!(Complex<f32>, Complex<f32>, SDSP_CC32);
 pair!(f64, f64, SDSP_RR64);
 pair!(f64, Complex<f64>, SDSP_RC64);
 pair!(Complex<f64>, Complex<f64>, SDSP_CC64);
+
+macro_rules! iir_pair {
+    ($c:ty, $i:ty) => {
+        impl SdspIirPair for ($c, $i) {
+            type Coef = $c;
+            fn coef_from_f64(v: f64) -> $c {
+                v as $c
+            }
+        }
+    };
+}
+iir_pair!(f32, f32);
+iir_pair!(f32, Complex<f32>);
+iir_pair!(f64, f64);
+iir_pair!(f64, Complex<f64>);

@@ -1,9 +1,12 @@
 //! `solid` (juliantos/solid-dsp) streaming hot path on MI355X: the public types of
 //! `src/filter/*`, `src/dot_product/*` and `src/fft/*` with the same names and
-//! signatures, executed by libsdsp.so (include/sdsp.h).
+//! signatures (tests/test_rust_shim_api.py checks every `pub fn` against the
+//! reference), executed by libsdsp.so (include/sdsp.h).  Device-only extras are
+//! in `sdsp`.
 pub mod dot_product;
 pub mod fft;
 pub mod filter;
+pub mod sdsp;
 pub mod sys;
 
 use std::error::Error;

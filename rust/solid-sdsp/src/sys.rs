@@ -21,6 +21,9 @@ pub const SDSP_ALGO_EXACT: c_int = 1;
 pub const SDSP_ALGO_FMA: c_int = 2;
 pub const SDSP_ALGO_FFT: c_int = 3;
 
+pub const SDSP_TUNE_HOST_STEP: c_int = 16;
+pub const SDSP_TUNE_HOST_BLOCK_MACS: c_int = 17;
+
 pub const SDSP_OK: c_int = 0;
 pub const SDSP_E_COEFFICIENTS_LENGTH_ZERO: c_int = 1;
 pub const SDSP_E_DECIMATION_LESS_THAN_ONE: c_int = 2;
@@ -46,6 +49,10 @@ extern "C" {
     pub fn sdsp_fir_destroy(h: *mut sdsp_fir);
     pub fn sdsp_fir_clone(h: *const sdsp_fir, out: *mut *mut sdsp_fir) -> c_int;
     pub fn sdsp_fir_set_algo(h: *mut sdsp_fir, algo: c_int) -> c_int;
+    pub fn sdsp_fir_set_tuning(h: *mut sdsp_fir, key: c_int, value: c_int) -> c_int;
+    pub fn sdsp_fir_execute(h: *mut sdsp_fir, sample: *const c_void, out: *mut c_void, n_out: *mut usize) -> c_int;
+    pub fn sdsp_fir_get_state(h: *const sdsp_fir, hist: *mut c_void, phase: *mut usize) -> c_int;
+    pub fn sdsp_fir_synchronize(h: *mut sdsp_fir) -> c_int;
     pub fn sdsp_fir_set_scale(h: *mut sdsp_fir, scale: *const c_void) -> c_int;
     pub fn sdsp_fir_get_scale(h: *const sdsp_fir, scale: *mut c_void) -> c_int;
     pub fn sdsp_fir_len(h: *const sdsp_fir) -> usize;
@@ -97,6 +104,12 @@ extern "C" {
     pub fn sdsp_iir_execute_block(h: *mut sdsp_iir, input: *const c_void, n: usize, out: *mut c_void,
                                   n_out: *mut usize) -> c_int;
     pub fn sdsp_iir_reset(h: *mut sdsp_iir) -> c_int;
+    pub fn sdsp_iir_execute(h: *mut sdsp_iir, sample: *const c_void, out: *mut c_void, n_out: *mut usize) -> c_int;
+    pub fn sdsp_iir_num_coefs(h: *const sdsp_iir, which: c_int) -> usize;
+    pub fn sdsp_iir_coefficients(h: *const sdsp_iir, num: *mut f64, den: *mut f64) -> c_int;
+    pub fn sdsp_sos_section_coefs(h: *const sdsp_iir, section: c_int, num2: *mut f64, den3: *mut f64) -> c_int;
+    pub fn sdsp_iir_group_delay_taps(b: *const f64, nb: usize, a: *const f64, na: usize, f: f64,
+                                     out: *mut f64) -> c_int;
     pub fn sdsp_iir_frequency_response(h: *const sdsp_iir, f: f64, re_im: *mut f64) -> c_int;
     pub fn sdsp_iir_group_delay(h: *const sdsp_iir, f: f64, delay: *mut f64) -> c_int;
 
@@ -111,6 +124,13 @@ extern "C" {
     pub fn sdsp_chan_destroy(h: *mut sdsp_chan);
     pub fn sdsp_chan_execute_block(h: *mut sdsp_chan, input: *const c_void, n: usize, out: *mut c_void,
                                    frames: *mut usize) -> c_int;
+
+    // tap / loop-filter design (firdes/mod.rs:243-368, iirdes/pll/mod.rs:24-99)
+    pub fn sdsp_kaiser_beta(stop_band_attenuation: f64) -> f64;
+    pub fn sdsp_firdes_kaiser(n: usize, fc: f64, as_: f64, mu: f64, h: *mut f64) -> c_int;
+    pub fn sdsp_firdes_notch(m: usize, f0: f64, as_: f64, h: *mut f64) -> c_int;
+    pub fn sdsp_active_lag(bw: f64, zeta: f64, k: f64, num3: *mut f64, den3: *mut f64) -> c_int;
+    pub fn sdsp_active_proportional_integral(bw: f64, zeta: f64, k: f64, num3: *mut f64, den3: *mut f64) -> c_int;
 
     // DotProduct (dot_product/mod.rs:37-171)
     pub fn sdsp_dot_execute(dtype: c_int, coefs: *const c_void, len: usize, direction: c_int,

@@ -18,6 +18,8 @@ LIB_PATH = os.path.join(PKG, "_build", "libsdsp.so")
 # sdsp_dtype (Coef, In)
 RR32, RC32, CC32, RR64, RC64, CC64 = range(6)
 ALGO_AUTO, ALGO_EXACT, ALGO_FMA, ALGO_FFT = range(4)
+# sdsp_tune_key values used by the bindings (include/sdsp.h)
+TUNE_HOST_STEP, TUNE_HOST_BLOCK_MACS = 16, 17
 
 _PAIRS = {
     (np.dtype(np.float32), np.dtype(np.float32)): RR32,

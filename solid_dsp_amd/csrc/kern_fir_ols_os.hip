@@ -240,6 +240,240 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         if (r >= h2) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, 0);
 }
 
+#ifdef SDSP_OLS_LAB  // lab only: measured slower than the one-shot kernel
+// ---------------------------------------------------------------------------
+// Slot kernel: the same segment transform (bit-identical to ols_os_segment<0>),
+// persistent, one workgroup of SLOTS x 256 lanes per CU.  Slot s (waves
+// 4s..4s+3) takes its segments one at a time from its XCD eighth's counter
+// (workgroup b serves eighth b % 8; one returning device atomic per segment,
+// fetched a segment ahead), so the chip-wide window of segments in flight stays
+// as compact as the one-shot kernel's dispatch order.  What the shape buys: a
+// slot issues the loads of its next segment BEFORE the stores of the current
+// one (loads, stores and atomics retire in issue order per wave, so a wave that
+// loads after storing waits for its stores), and the two cross-wave phase
+// boundaries are slot-local LDS counters (no slot waits for another).
+//
+// Per-slot LDS: the 34 KB image of ols_os_segment.  Column t of the image is
+// owned by lane t of the slot in P1 and P5, so segment i + 1's P1 may start
+// while other waves of the slot still run segment i's P5.
+template <int SLOTS>
+struct OlsSlotShared {
+    f2 img[SLOTS][16 * kRow];
+    unsigned bar[SLOTS];      // slot barrier arrivals (monotonic)
+    long long nxt[SLOTS][2];  // next segment of the slot, double-buffered by parity
+    unsigned tk_next, tk_done;  // load tickets (FIFO): at most `tok` waves with segment loads in flight
+};
+
+__device__ __forceinline__ void tok_acquire(unsigned* next, const unsigned* done, int tok) {
+    if (tok <= 0) return;
+    unsigned my = 0;
+    if ((threadIdx.x & 63) == 0) my = __hip_atomic_fetch_add(next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    my = __builtin_amdgcn_readfirstlane(my);
+    for (int spin = 0; __builtin_amdgcn_readfirstlane(__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) +
+                               (unsigned)tok <= my && spin < (1 << 22);
+         ++spin)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void tok_release(unsigned* done, int tok) {
+    if (tok <= 0) return;
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// every wait is bounded (~2^22 x 64 cycles): a protocol error can never hang the GPU
+constexpr int kSpinLimit = 1 << 22;
+
+__device__ __forceinline__ unsigned lds_poll(const unsigned* p) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+
+// all 4 waves of a slot: this wave's LDS writes are complete before it arrives;
+// no LDS access of the caller moves across the call.  false: the bounded wait ran
+// out (a protocol error) -- the caller stops, it never goes on with unsynchronised data
+__device__ __forceinline__ bool slot_barrier(unsigned* ctr, unsigned target) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int spin = 0;
+    for (; lds_poll(ctr) < target && spin < kSpinLimit; ++spin) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    return spin < kSpinLimit;
+}
+
+// ABL (lab builds only): 1 HBM traffic only (rows stored as loaded), 2 compute only (no loads, no stores)
+template <int SLOTS, int ABL = 0>
+__global__ void __launch_bounds__(256 * SLOTS, 1)
+fir_ols_slot_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
+                    f2* __restrict__ y, long long n, long long lo, long long hi, long long q, int h2,
+                    unsigned long long* __restrict__ queue, int tok) {
+    __shared__ __attribute__((aligned(16))) OlsSlotShared<SLOTS> sh;
+    const int slot = threadIdx.x >> 8, t = threadIdx.x & 255;
+    const int hi4 = t >> 4, lo4 = t & 15;
+    const int xc = blockIdx.x & 7;
+    const long long s0 = lo + (long long)xc * q, xe0 = lo + (long long)(xc + 1) * q, xe = xe0 < hi ? xe0 : hi;
+    const long long cnt = xe > s0 ? xe - s0 : 0;
+    const int V = 4096 - 256 * h2;
+    const long long chan = (long long)blockIdx.y * n;
+    unsigned long long* qc = queue + 16 * (8 * blockIdx.y + xc);  // [channel][eighth], 128 bytes apart
+
+    const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
+    const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0, 2048 * 16, kBufWord3);
+    f2* img = sh.img[slot];
+    f2* col = img + t + (t >> 4);
+    f2* r2 = img + hi4 * kRow + lo4;
+    unsigned* bar = &sh.bar[slot];
+    unsigned nbar = 0;
+
+    if (threadIdx.x < SLOTS) sh.bar[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sh.tk_next = sh.tk_done = 0;
+    if (t == 0) sh.nxt[slot][0] = (long long)__hip_atomic_fetch_add(qc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // the only workgroup barrier before the tail
+
+    // loop-invariant twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build)
+    const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 0, 0));
+    const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 4096, 0));
+    const float4 b2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 8192, 0));
+    f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
+    f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
+
+    long long k = __builtin_amdgcn_readfirstlane((int)sh.nxt[slot][0]);  // index within the eighth
+    if (k < 0) k = cnt;
+    unsigned long long fetched = 0;
+    if (t == 0) fetched = __hip_atomic_fetch_add(qc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f2 v[16];
+    if (k < cnt) tok_acquire(&sh.tk_next, &sh.tk_done, tok);
+    {
+        const bool any = k < cnt;
+        const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + chan + (s0 + (any ? k : 0)) * V - 256 * h2),
+                                                          (short)0, any ? 32768 : 0, kBufWord3);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if constexpr (ABL == 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)k};
+            else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+        // 16 dropped stores (empty descriptor): the loop is entered with 16 vector-memory operations younger
+        // than the segment loads on every path, so the waits at the top of the loop let a previous
+        // segment's stores stay in flight (vmcnt counts loads and stores together, in issue order)
+        const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 0, kBufWord3);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rz, 8 * t, 2048 * r, 0);
+    }
+    for (long long it = 0; k < cnt; ++it) {  // k uniform over the slot
+        const long long base = chan + (s0 + k) * V - 256 * h2;
+        if constexpr (ABL == 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) asm volatile("" ::"v"(v[r]));  // the loads have landed
+            tok_release(&sh.tk_done, tok);
+            if (t == 0) sh.nxt[slot][(it + 1) & 1] = (long long)fetched;
+            if (!slot_barrier(bar, 4 * ++nbar) || !slot_barrier(bar, 4 * ++nbar)) break;
+        } else {
+        // P1: DFT16 n2 -> k0, * W4096^(t k0) -> (k0, t)
+        pdft16<false>(v);
+        tok_release(&sh.tk_done, tok);  // the segment's loads have landed
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) col[kk * kRow] = kk == 0 ? v[0] : pmul(v[kout(kk)], tw_pair(Cb, Da, kk));
+        if (t == 0) sh.nxt[slot][(it + 1) & 1] = (long long)fetched;  // read after barrier 2
+        if (!slot_barrier(bar, 4 * ++nbar)) break;
+
+        // P2, P3, P4 (wave-local rows)
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) v[jj] = r2[17 * jj];
+        float4 hq[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+        const float4 e0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12288, 0));
+        const float4 e1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12544, 0));
+        const float4 e2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12800, 0));
+        const f2 Eb[3] = {f2{e0.x, e0.y}, f2{e0.z, e0.w}, f2{e1.x, e1.y}};
+        const f2 Fa[3] = {f2{e1.z, e1.w}, f2{e2.x, e2.y}, f2{e2.z, e2.w}};
+        f2 w2[16];
+#pragma unroll
+        for (int kk = 1; kk < 16; ++kk) w2[kk] = tw_pair(Eb, Fa, kk);
+        pdft16<false>(v);
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) r2[17 * kk] = kk == 0 ? v[0] : pmul(v[kout(kk)], w2[kk]);
+        phase_sync<true>();
+        {
+            f2* r3 = img + hi4 * kRow + 17 * lo4;
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) v[jj] = r3[jj];
+            pdft16<false>(v);
+            f2 u[16];
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                u[2 * p] = pmul(v[kout(2 * p)], f2{hq[p].x, hq[p].y});
+                u[2 * p + 1] = pmul(v[kout(2 * p + 1)], f2{hq[p].z, hq[p].w});
+            }
+            pdft16<true>(u);
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) r3[jj] = jj == 0 ? u[kout(0)] : pmulc(u[kout(jj)], w2[jj]);
+        }
+        phase_sync<true>();
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) v[jj] = r2[17 * jj];
+        pdft16<true>(v);
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) r2[17 * kk] = v[kout(kk)];
+        if (!slot_barrier(bar, 4 * ++nbar)) break;
+
+        // P5: * conj W4096^(t k0), IDFT16 k0 -> n2; row n2 at v[kout(n2)]
+#pragma unroll
+        for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Cb[i]), "+v"(Da[i]));
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) v[kk] = kk == 0 ? col[0] : pmulc(col[kk * kRow], tw_pair(Cb, Da, kk));
+        pdft16<true>(v);
+        }
+        // next segment: index, its loads and the fetch of the one after, issued before this segment's stores
+        long long kn = __builtin_amdgcn_readfirstlane((int)sh.nxt[slot][(it + 1) & 1]);
+        if (kn < 0) kn = cnt;
+        if (t == 0 && kn < cnt) fetched = __hip_atomic_fetch_add(qc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        f2 vn[16];
+        if (kn < cnt) tok_acquire(&sh.tk_next, &sh.tk_done, tok);  // released after its P1
+        {  // past the last segment: an empty descriptor (the loads return 0 without touching memory)
+            const bool more = kn < cnt;
+            const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + chan + (s0 + (more ? kn : k)) * V - 256 * h2),
+                                                              (short)0, more ? 32768 : 0, kBufWord3);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if constexpr (ABL == 2) vn[r] = f2{1e-3f * t + r, 1e-9f * (float)kn};
+                else vn[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+        }
+
+        // halo rows (r < h2) go to an empty descriptor: the store is dropped, every row issues one store
+        const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, 32768, kBufWord3);
+        const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, 0, kBufWord3);
+        if constexpr (ABL == 2) {
+            f2 acc = v[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) acc += v[r];
+            if (acc.x == 1.2345e30f) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc), ry, 8 * t, 0, 0);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[ABL == 1 ? r : kout(r)]), r >= h2 ? ry : rz,
+                                                      8 * t, 2048 * r, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = vn[r];
+        k = kn;
+    }
+    // the last workgroup to finish rewinds the counters for the next launch (stream order)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long total = (unsigned long long)gridDim.x * gridDim.y;
+        unsigned long long* done = queue + 16 * 8 * gridDim.y;
+        if (__hip_atomic_fetch_add(done, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+            for (unsigned i = 0; i < 8 * gridDim.y; ++i)
+                __hip_atomic_store(queue + 16 * i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+#endif  // SDSP_OLS_LAB
+
+#ifdef SDSP_OLS_LAB
+__device__ unsigned long long g_ols_lab_queue[16 * 8 + 16];
+#endif
+
 template <int VAR>
 __global__ void __launch_bounds__(256, 4)
 fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
@@ -254,10 +488,11 @@ fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const
 }
 
 #ifdef SDSP_OLS_LAB
-static int g_lab_variant = 0, g_lab_lds = 0;
-extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int lds, int) {
+static int g_lab_variant = 0, g_lab_lds = 0, g_lab_tok = 0;
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int lds, int tok) {
     g_lab_variant = v;
     g_lab_lds = lds;
+    g_lab_tok = v >= 256 && tok > 1 ? tok : 0;  // slot kernel: waves with loads in flight per CU (chunk field)
 }
 __global__ void ols_hwid_probe_kernel(unsigned int* out) {
     unsigned int xcc, hw;
@@ -282,6 +517,30 @@ hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n,
     const long long q = (hi - lo + 7) / 8;
     const dim3 grid((unsigned)(8 * q), (unsigned)channels);
 #ifdef SDSP_OLS_LAB
+    if (g_lab_variant >= 256) {  // slot kernel: 256 + 16 ablation + SLOTS (3 or 4); lds field = workgroups per eighth
+        const int slots = g_lab_variant & 15;
+        const int J = g_lab_lds > 0 ? g_lab_lds : 32;
+        const dim3 g2(8 * J, (unsigned)channels);
+        if (channels != 1) return hipErrorInvalidValue;
+        unsigned long long* qp = nullptr;
+        hipGetSymbolAddress((void**)&qp, HIP_SYMBOL(g_ols_lab_queue));
+        const int abl = (g_lab_variant >> 4) & 3;
+        if (slots == 4 && abl == 1)
+            hipLaunchKernelGGL((fir_ols_slot_kernel<4, 1>), g2, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows, qp, g_lab_tok);
+        else if (slots == 4 && abl == 2)
+            hipLaunchKernelGGL((fir_ols_slot_kernel<4, 2>), g2, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows, qp, g_lab_tok);
+        else if (slots == 4)
+            hipLaunchKernelGGL((fir_ols_slot_kernel<4>), g2, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows, qp, g_lab_tok);
+        else if (slots == 3)
+            hipLaunchKernelGGL((fir_ols_slot_kernel<3>), g2, dim3(768), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows, qp, g_lab_tok);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
 #define SDSP_LAB_CASE(V)                                                                                       \
     if (g_lab_variant == V) {                                                                                  \
         hipLaunchKernelGGL(fir_ols_os_kernel<V>, grid, dim3(256), g_lab_lds, s, (const f2*)x,                  \

@@ -43,7 +43,10 @@ fir_step_kernel(I sample, const I* __restrict__ hist_in, I* __restrict__ hist_ou
     }
     // the new delay line: the last Lm1 of (hist_in, sample)
     for (int k = t; k < Lm1; k += kStepThreads) hist_out[k] = k + 1 < Lm1 ? hist_in[k + 1] : sample;
-    if (t == 0 && flag) __hip_atomic_store(flag, seq + (unsigned)t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // every wave's delay-line stores happen before the flag (the host may start the next
+    // device call as soon as it sees it): workgroup barrier, then a system-scope release
+    __syncthreads();
+    if (t == 0 && flag) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <typename C, typename I>

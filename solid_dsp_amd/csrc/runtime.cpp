@@ -96,8 +96,16 @@ struct sdsp_fir {
     hipStream_t stream = nullptr;
     mutable StreamFence fence;         // last stream an execute call was queued on
     DevBuf stage_in, stage_out;
-    HostMapped step_out;  // per-sample execute: output at [0, 16), completion flag at [16, 20)
+    HostMapped step_out;  // per-sample execute on the device: output at [0, 16), completion flag at [16, 20)
     unsigned step_seq = 0;
+    // host delay line for per-sample calls and small host blocks (runtime_host_step below):
+    // hbuf holds 2(L-1) samples, the window (oldest first) is hbuf[hpos, hpos + L-1)
+    std::vector<unsigned char> hbuf;
+    size_t hpos = 0;
+    bool host_valid = false;  // hbuf holds the current window (single-channel handles only)
+    bool dev_stale = false;   // the host consumed samples after d_hist[cur] was last written
+    int host_step = 1;        // SDSP_TUNE_HOST_STEP
+    size_t host_macs = 1u << 16;  // host blocks: n * L up to this many multiply-adds
     // overlap-save plan
     bool ols_ok = false;
     int ols_kernel = kOlsOneShot;  // SDSP_TUNE_OLS_KERNEL
@@ -118,6 +126,11 @@ int fir_alloc_state(sdsp_fir* h) {
     h->cur = 0;
     h->ci = 0;
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    const size_t lm1 = h->L - 1, sb = sample_bytes(h->dtype);
+    h->hbuf.assign(2 * lm1 * sb, 0);  // the zeroed window, both copies
+    h->hpos = 0;
+    h->host_valid = h->channels == 1;
+    h->dev_stale = false;
     return SDSP_OK;
 }
 
@@ -294,6 +307,190 @@ int fir_create_common(sdsp_fir** out, int dtype, const void* taps, size_t len, c
 
 }  // namespace
 
+namespace {
+// ---------------------------------------------------------------------------
+// Host step: Filter::execute(sample), DecimatingFIRFilter::push and small host
+// blocks run on the host against the handle's own delay line, in
+// the reference's arithmetic (fir/mod.rs:209-212, decim.rs:115-118, 221-228:
+// acc = 0; acc += cr[i] x[n-i] for i = 0..L-1; y = acc * scale; num-complex
+// products, no contraction -- this TU is built with -ffp-contract=off).  It is
+// the product's own small-work path, not a fallback: creating a handle still
+// requires the gfx950 device, and every block above the threshold runs on it.
+// Coherence: the state is the last L-1 inputs, so it moves between host and
+// device only when the side that runs next does not hold it -- one D2H of L-1
+// samples before the first host step after device work (host_pull), one H2D
+// before the first device call after host steps (host_flush).
+template <typename T> struct hcx {
+    T re, im;
+};
+template <typename T> inline T hmul(T a, T b) { return a * b; }
+template <typename T> inline hcx<T> hmul(T a, hcx<T> b) { return {a * b.re, a * b.im}; }
+template <typename T> inline hcx<T> hmul(hcx<T> a, T b) { return {a.re * b, a.im * b}; }
+template <typename T> inline hcx<T> hmul(hcx<T> a, hcx<T> b) {
+    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+template <typename T> inline T hadd(T a, T b) { return a + b; }
+template <typename T> inline hcx<T> hadd(hcx<T> a, hcx<T> b) { return {a.re + b.re, a.im + b.im}; }
+// fused forms: fmac_ of sdsp_device.hpp (the device FMA kernels), one rounding per fma
+inline float hfma(float acc, float c, float x) { return std::fma(c, x, acc); }
+inline double hfma(double acc, double c, double x) { return std::fma(c, x, acc); }
+template <typename T> inline hcx<T> hfma(hcx<T> acc, T c, hcx<T> x) { return {hfma(acc.re, c, x.re), hfma(acc.im, c, x.im)}; }
+template <typename T> inline hcx<T> hfma(hcx<T> acc, hcx<T> c, hcx<T> x) {
+    return {hfma(hfma(acc.re, c.re, x.re), -c.im, x.im), hfma(hfma(acc.im, c.re, x.im), c.im, x.re)};
+}
+template <typename T> inline T hzero() { return T{}; }
+
+template <typename C, typename I>
+void host_step_t(sdsp_fir* h, const unsigned char* sample, unsigned char* out, bool emit, bool fused) {
+    const size_t L = h->L, lm1 = L - 1;
+    I x;
+    std::memcpy(&x, sample, sizeof(I));
+    I* b = reinterpret_cast<I*>(h->hbuf.data());
+    if (emit) {
+        const I* w = b + h->hpos;  // window oldest first: x[n - i] = w[lm1 - i]
+        const C* taps = reinterpret_cast<const C*>(h->taps.data());  // cr[i] = h[L-1-i]
+        I acc = hzero<I>();
+        if (fused) {
+            acc = hfma(acc, taps[L - 1], x);
+            for (size_t i = 1; i < L; ++i) acc = hfma(acc, taps[L - 1 - i], w[lm1 - i]);
+        } else {
+            acc = hadd(acc, hmul(taps[L - 1], x));
+            for (size_t i = 1; i < L; ++i) acc = hadd(acc, hmul(taps[L - 1 - i], w[lm1 - i]));
+        }
+        C sc;
+        std::memcpy(&sc, h->scale.data(), sizeof(C));
+        const I y = hmul(acc, sc);
+        std::memcpy(out, &y, sizeof(I));
+    }
+    if (lm1) {  // Window::push (src/window/mod.rs:36-41) on the doubled buffer
+        b[h->hpos] = x;
+        b[h->hpos + lm1] = x;
+        h->hpos = h->hpos + 1 == lm1 ? 0 : h->hpos + 1;
+    }
+}
+
+void host_step(sdsp_fir* h, const unsigned char* sample, unsigned char* out, bool emit) {
+    const bool fused = h->algo == SDSP_ALGO_FMA;
+    switch (h->dtype) {
+        case SDSP_RR32: return host_step_t<float, float>(h, sample, out, emit, fused);
+        case SDSP_RC32: return host_step_t<float, hcx<float>>(h, sample, out, emit, fused);
+        case SDSP_CC32: return host_step_t<hcx<float>, hcx<float>>(h, sample, out, emit, fused);
+        case SDSP_RR64: return host_step_t<double, double>(h, sample, out, emit, fused);
+        case SDSP_RC64: return host_step_t<double, hcx<double>>(h, sample, out, emit, fused);
+        case SDSP_CC64: return host_step_t<hcx<double>, hcx<double>>(h, sample, out, emit, fused);
+    }
+}
+
+// the host window := the device history (after device work)
+int host_pull(sdsp_fir* h) {
+    if (h->host_valid) return SDSP_OK;
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
+    SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    const size_t lm1 = h->L - 1, sb = sample_bytes(h->dtype);
+    h->hbuf.resize(2 * lm1 * sb);
+    if (lm1) {
+        SDSP_TRY(hipMemcpy(h->hbuf.data(), h->d_hist[h->cur].p, lm1 * sb, hipMemcpyDeviceToHost), "pull history");
+        std::memcpy(h->hbuf.data() + lm1 * sb, h->hbuf.data(), lm1 * sb);
+    }
+    h->hpos = 0;
+    h->host_valid = true;
+    return SDSP_OK;
+}
+
+// the device history := the host window (before device work after host steps).  No
+// kernel can be reading d_hist here: host steps start only after host_pull's
+// synchronisation, a synchronising host call, or a state reset.
+int host_flush(const sdsp_fir* hc) {
+    sdsp_fir* h = const_cast<sdsp_fir*>(hc);
+    if (!h->dev_stale) return SDSP_OK;
+    const size_t lm1 = h->L - 1, sb = sample_bytes(h->dtype);
+    if (lm1)
+        SDSP_TRY(hipMemcpy(h->d_hist[h->cur].p, h->hbuf.data() + h->hpos * sb, lm1 * sb, hipMemcpyHostToDevice),
+                 "flush history");
+    h->dev_stale = false;
+    return SDSP_OK;
+}
+
+// keep a valid host window current across a device block whose input the host holds
+void host_feed(sdsp_fir* h, const unsigned char* in, size_t n) {
+    const size_t lm1 = h->L - 1, sb = sample_bytes(h->dtype);
+    if (!h->host_valid || !lm1 || !n) return;
+    if (n >= lm1) {
+        std::memcpy(h->hbuf.data(), in + (n - lm1) * sb, lm1 * sb);
+        std::memcpy(h->hbuf.data() + lm1 * sb, in + (n - lm1) * sb, lm1 * sb);
+        h->hpos = 0;
+        return;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        std::memcpy(h->hbuf.data() + h->hpos * sb, in + i * sb, sb);
+        std::memcpy(h->hbuf.data() + (h->hpos + lm1) * sb, in + i * sb, sb);
+        h->hpos = h->hpos + 1 == lm1 ? 0 : h->hpos + 1;
+    }
+}
+
+bool host_eligible(const sdsp_fir* h, size_t n) {
+    return h->host_step && h->channels == 1 && h->algo != SDSP_ALGO_FFT && n * h->L <= h->host_macs;
+}
+
+// n inputs through the host step; outputs (when `out`) where the phase emits (decim.rs:221-228)
+int host_run(sdsp_fir* h, const unsigned char* in, size_t n, unsigned char* out, size_t* n_out) {
+    int st = host_pull(h);
+    if (st) return st;
+    const size_t sb = sample_bytes(h->dtype);
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const bool emit = out && (h->M == 1 || (h->M - 1 - h->ci) % h->M == 0);
+        host_step(h, in + i * sb, emit ? out + k * sb : nullptr, emit);
+        h->ci = (h->ci + 1) % h->M;
+        k += emit;
+    }
+    if (n) h->dev_stale = true;
+    if (n_out) *n_out = k;
+    return SDSP_OK;
+}
+
+// one input through the single-launch device step kernel (kern_fir_step.hip,
+// SDSP_TUNE_HOST_STEP = 0): the delay line shifts on the device, the output (when
+// the phase emits and `want` is set) lands in host-mapped memory
+int fir_step_device(sdsp_fir* h, const void* sample, void* out, size_t* n_out, bool want) {
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
+    int st = host_flush(h);
+    if (st) return st;
+    if (!h->step_out.host) {
+        SDSP_TRY(h->step_out.ensure(32), "alloc mapped output");
+        std::memset(h->step_out.host, 0, 32);  // pinned memory is not zeroed: no stale flag value
+    }
+    const bool emit = want && (h->M == 1 || (h->M - 1 - h->ci) % h->M == 0);  // decim.rs:221-231
+    unsigned* flag_h = reinterpret_cast<unsigned*>((char*)h->step_out.host + 16);
+    unsigned seq = ++h->step_seq;
+    if (seq == 0) seq = h->step_seq = 1;  // the flag's initial 0 never matches
+    FirStepArgs a{sample, h->d_hist[h->cur].p, h->d_hist[h->cur ^ 1].p, h->d_taps_rev.p, h->scale.data(),
+                  h->step_out.dev, reinterpret_cast<unsigned*>((char*)h->step_out.dev + 16), seq, (int)h->L - 1,
+                  (int)h->L, emit, h->algo != SDSP_ALGO_FMA};
+    SDSP_TRY(launch_fir_step(h->dtype, a, h->stream), "fir step");
+    h->cur ^= 1;
+    h->ci = (h->ci + 1) % h->M;
+    h->host_valid = false;
+    // the flag is released after the whole workgroup's delay-line stores; the fence orders any
+    // later launch on a caller stream after the kernel itself
+    SDSP_TRY(h->fence.record(h->stream), "record fence");
+    SDSP_TRY(wait_host_flag(flag_h, seq, h->stream), "fir step wait");
+    if (emit && out) std::memcpy(out, h->step_out.host, sample_bytes(h->dtype));
+    if (n_out) *n_out = emit ? 1 : 0;
+    return SDSP_OK;
+}
+
+int fir_step(sdsp_fir* h, const void* sample, void* out, size_t* n_out, bool want) {
+    if (!h || !sample || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
+    DeviceGuard g(h->device);
+    if (!h->host_step) return fir_step_device(h, sample, out, n_out, want);
+    size_t k = 0;
+    int st = host_run(h, (const unsigned char*)sample, 1, want ? (unsigned char*)out : nullptr, &k);
+    if (n_out) *n_out = k;
+    return st;
+}
+}  // namespace
+
 extern "C" {
 
 const char* sdsp_last_error(void) { return g_last_error.c_str(); }
@@ -325,6 +522,7 @@ void sdsp_fir_destroy(sdsp_fir* h) {
     if (!h) return;
     {
         DeviceGuard g(h->device);
+        (void)h->fence.wait();  // work queued on a caller stream may still read the tables / history
         if (h->stream) {
             (void)hipStreamSynchronize(h->stream);
             (void)hipStreamDestroy(h->stream);
@@ -374,6 +572,19 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
             if (value < 0) return SDSP_E_INVALID_ARGUMENT;
             h->decim_seg = value;
             return SDSP_OK;
+        case SDSP_TUNE_HOST_STEP:
+            if (value < 0 || value > 1) return SDSP_E_INVALID_ARGUMENT;
+            if (!value) {  // the device kernels take over: they need the newest window
+                DeviceGuard g(h->device);
+                int st = host_flush(h);
+                if (st) return st;
+            }
+            h->host_step = value;
+            return SDSP_OK;
+        case SDSP_TUNE_HOST_BLOCK_MACS:
+            if (value < 0) return SDSP_E_INVALID_ARGUMENT;
+            h->host_macs = (size_t)value;
+            return SDSP_OK;
         default:
             set_error("unknown or retired tuning key");
             return SDSP_E_INVALID_ARGUMENT;
@@ -396,9 +607,14 @@ int sdsp_fir_clone(const sdsp_fir* h, sdsp_fir** out) {
     const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
     SDSP_TRY(h->fence.wait(), "wait for queued work");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    st = host_flush(h);
+    if (st) return st;
     if (hb) SDSP_TRY(hipMemcpy(c->d_hist[0].p, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToDevice), "clone state");
     c->cur = 0;
     c->ci = h->ci;
+    c->host_step = h->host_step;
+    c->host_macs = h->host_macs;
+    c->host_valid = false;
     return SDSP_OK;
 }
 
@@ -446,6 +662,11 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
         set_error("input and output blocks overlap (in-place filtering is not supported)");
         return SDSP_E_INVALID_ARGUMENT;
     }
+    int hst = host_flush(h);
+    if (hst) return hst;
+    h->host_valid = false;  // the input is device-resident: the host window is re-read when needed
+    // work queued on another stream (the fence) reads or writes the history this launch uses
+    if (h->fence.pending) SDSP_TRY(hipStreamWaitEvent(s, h->fence.ev, 0), "order after queued work");
     const void* hist = h->d_hist[h->cur].p;
     if (h->M == 1) {
         const int algo = fir_resolve_algo(h, n);
@@ -484,6 +705,8 @@ int sdsp_fir_execute_block(sdsp_fir* h, const void* in, size_t n, void* out, siz
     const size_t nout = sdsp_fir_output_count(h, n);
     if (n_out) *n_out = nout;
     if (n == 0) return SDSP_OK;
+    if (host_eligible(h, n)) return host_run(h, (const unsigned char*)in, n, (unsigned char*)out, nullptr);
+    const bool keep = h->host_valid;
     SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
     SDSP_TRY(h->stage_out.ensure(h->channels * std::max<size_t>(nout, 1) * sb), "stage out");
     SDSP_TRY(hipMemcpyAsync(h->stage_in.p, in, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
@@ -493,33 +716,10 @@ int sdsp_fir_execute_block(sdsp_fir* h, const void* in, size_t n, void* out, siz
         SDSP_TRY(hipMemcpyAsync(out, h->stage_out.p, h->channels * nout * sb, hipMemcpyDeviceToHost, h->stream),
                  "D2H");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    h->host_valid = keep;  // the host holds the input: move its window on without a read-back
+    host_feed(h, (const unsigned char*)in, n);
     return SDSP_OK;
 }
-
-namespace {
-// one input through the single-launch step kernel (kern_fir_step.hip): the
-// delay line shifts on the device, the output (when the phase emits and
-// `want` is set) lands in host-mapped memory -- one launch, one sync, no copies
-int fir_step(sdsp_fir* h, const void* sample, void* out, size_t* n_out, bool want) {
-    if (!h || !sample || h->channels != 1) return SDSP_E_INVALID_ARGUMENT;
-    DeviceGuard g(h->device);
-    SDSP_TRY(h->fence.wait(), "wait for queued work");
-    SDSP_TRY(h->step_out.ensure(32), "alloc mapped output");
-    const bool emit = want && (h->M == 1 || (h->M - 1 - h->ci) % h->M == 0);  // decim.rs:221-231
-    unsigned* flag_h = reinterpret_cast<unsigned*>((char*)h->step_out.host + 16);
-    const unsigned seq = ++h->step_seq;
-    FirStepArgs a{sample, h->d_hist[h->cur].p, h->d_hist[h->cur ^ 1].p, h->d_taps_rev.p, h->scale.data(),
-                  h->step_out.dev, reinterpret_cast<unsigned*>((char*)h->step_out.dev + 16), seq, (int)h->L - 1,
-                  (int)h->L, emit, h->algo != SDSP_ALGO_FMA};
-    SDSP_TRY(launch_fir_step(h->dtype, a, h->stream), "fir step");
-    h->cur ^= 1;
-    h->ci = (h->ci + 1) % h->M;
-    SDSP_TRY(wait_host_flag(flag_h, seq, h->stream), "fir step wait");
-    if (emit && out) std::memcpy(out, h->step_out.host, sample_bytes(h->dtype));
-    if (n_out) *n_out = emit ? 1 : 0;
-    return SDSP_OK;
-}
-}  // namespace
 
 int sdsp_fir_execute(sdsp_fir* h, const void* sample, void* out, size_t* n_out) {
     if (!out) return SDSP_E_INVALID_ARGUMENT;
@@ -531,6 +731,9 @@ int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n) {
     if (n == 0) return SDSP_OK;
     DeviceGuard g(h->device);
     SDSP_TRY(h->fence.wait(), "wait for queued work");
+    if (host_eligible(h, n)) return host_run(h, (const unsigned char*)samples, n, nullptr, nullptr);
+    int hst = host_flush(h);
+    if (hst) return hst;
     const size_t sb = sample_bytes(h->dtype);
     SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
     SDSP_TRY(hipMemcpyAsync(h->stage_in.p, samples, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
@@ -540,6 +743,7 @@ int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n) {
     h->cur ^= 1;
     h->ci = (h->ci + n) % h->M;
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
+    host_feed(h, (const unsigned char*)samples, n);
     return SDSP_OK;
 }
 
@@ -562,7 +766,11 @@ int sdsp_fir_get_state(const sdsp_fir* h, void* hist, size_t* phase) {
     const size_t hb = h->channels * (h->L - 1) * sample_bytes(h->dtype);
     SDSP_TRY(h->fence.wait(), "wait for queued work");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
-    if (hb && hist) SDSP_TRY(hipMemcpy(hist, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToHost), "get state");
+    if (h->dev_stale) {  // the host window is the newer one
+        if (hb && hist) std::memcpy(hist, h->hbuf.data() + h->hpos * sample_bytes(h->dtype), hb);
+    } else if (hb && hist) {
+        SDSP_TRY(hipMemcpy(hist, h->d_hist[h->cur].p, hb, hipMemcpyDeviceToHost), "get state");
+    }
     if (phase) *phase = h->ci;
     return SDSP_OK;
 }
@@ -575,6 +783,8 @@ int sdsp_fir_set_state(sdsp_fir* h, const void* hist, size_t phase) {
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     if (hb && hist) SDSP_TRY(hipMemcpy(h->d_hist[h->cur].p, hist, hb, hipMemcpyHostToDevice), "set state");
     h->ci = phase;
+    h->dev_stale = false;
+    h->host_valid = false;  // re-read on the next host step
     return SDSP_OK;
 }
 
@@ -605,6 +815,7 @@ int sdsp_fir_group_delay(const sdsp_fir* h, double f, double* delay) {
 int sdsp_fir_synchronize(sdsp_fir* h) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     DeviceGuard g(h->device);
+    SDSP_TRY(h->fence.wait(), "wait for queued work");
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     return SDSP_OK;
 }

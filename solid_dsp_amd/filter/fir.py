@@ -35,7 +35,7 @@ class _FirBase:
     _decim = False
 
     def __init__(self, coefs, scale, decimation=1, sample_dtype=None, coef_dtype=None, device=0, channels=1,
-                 algo=None):
+                 algo=None, host_step=None):
         c = _coef_array(coefs, coef_dtype)
         if sample_dtype is None:
             sample_dtype = _default_sample(c.dtype)
@@ -56,6 +56,8 @@ class _FirBase:
             self.set_channels(channels)
         if algo is not None:  # default: the handle's ALGO_EXACT (bit-identical to the reference)
             self.set_algo(algo)
+        if host_step is not None:  # default: the handle's host step (sdsp.h SDSP_TUNE_HOST_STEP)
+            self.set_host_step(host_step)
 
     @classmethod
     def _wrap(cls, handle, dtype, channels, device=0):
@@ -81,6 +83,13 @@ class _FirBase:
 
     def set_algo(self, algo: int):
         L.check(L.lib().sdsp_fir_set_algo(self._h, algo))
+
+    def set_host_step(self, on: bool, block_macs: int = None):
+        """execute(sample), push and host blocks of n * len <= block_macs multiply-adds on the host
+        against the handle's delay line (True, the default) or as device launches (False)."""
+        L.check(L.lib().sdsp_fir_set_tuning(self._h, L.TUNE_HOST_STEP, 1 if on else 0))
+        if block_macs is not None:
+            L.check(L.lib().sdsp_fir_set_tuning(self._h, L.TUNE_HOST_BLOCK_MACS, int(block_macs)))
 
     def set_scale(self, scale):  # fir/mod.rs:103-106
         s = np.array([scale], dtype=self.coef_dtype)
@@ -182,8 +191,8 @@ class FIRFilter(_FirBase):
     """
 
     def __init__(self, coefs, scale=1.0, sample_dtype=None, coef_dtype=None, device=0, channels=1,
-                 algo=None):
-        super().__init__(coefs, scale, 1, sample_dtype, coef_dtype, device, channels, algo)
+                 algo=None, host_step=None):
+        super().__init__(coefs, scale, 1, sample_dtype, coef_dtype, device, channels, algo, host_step)
 
     @classmethod
     def new(cls, coefs, scale, **kw):
@@ -196,8 +205,8 @@ class DecimatingFIRFilter(_FirBase):
     _decim = True
 
     def __init__(self, coefs, scale=1.0, decimation=1, sample_dtype=None, coef_dtype=None, device=0,
-                 channels=1, algo=None):
-        super().__init__(coefs, scale, decimation, sample_dtype, coef_dtype, device, channels, algo)
+                 channels=1, algo=None, host_step=None):
+        super().__init__(coefs, scale, decimation, sample_dtype, coef_dtype, device, channels, algo, host_step)
 
     @classmethod
     def new(cls, coefs, scale, decimation, **kw):

@@ -67,10 +67,63 @@ def gather_full_to_root(out, root: int = 0, chunk_bytes: int = 1 << 30):
     out = out.reshape(-1)
     if not out.is_contiguous():
         raise ValueError("gather_full_to_root: output must be contiguous")
+    cplx = out.is_complex()
+    if cplx:  # neither gloo nor RCCL gathers complex dtypes: move the interleaved (re, im) pairs as reals
+        out = torch.view_as_real(out).reshape(-1)
     numel = out.numel()
     step = max(1, chunk_bytes // out.element_size())
+    if cplx:
+        step -= step % 2  # a chunk never splits a (re, im) pair
+        step = max(step, 2)
     big = torch.empty((world, numel), dtype=out.dtype, device=out.device) if rank == root else None
     for c0 in range(0, numel, step):
         c1 = min(numel, c0 + step)
         dist.gather(out[c0:c1], [big[r, c0:c1] for r in range(world)] if rank == root else None, dst=root)
+    if cplx and big is not None:
+        big = torch.view_as_complex(big.view(world, numel // 2, 2))
     return big
+
+
+# ---------------------------------------------------------------------------
+# Checking a gathered output (bench.py after the RCCL gather; the gloo dry run).
+# The index arithmetic lives here, testable without a GPU; the expected values
+# come from a caller-supplied function (bench.py passes the f64 restatement).
+
+def fir_input_window(s: int, width: int, taps: int):
+    """Inputs that determine FIR outputs [s, s + width) of a stream (y[n] uses
+    x[n - taps + 1 .. n], fir/mod.rs:209-212): (first input, input count, outputs of
+    a zero-state run over them to drop).  Needs s >= taps - 1."""
+    if s < taps - 1:
+        raise ValueError("window starts before the first full delay line")
+    return s - (taps - 1), width + taps - 1, taps - 1
+
+
+def decim_input_window(m: int, width: int, taps: int, M: int):
+    """Inputs that determine decimated outputs [m, m + width) of a stream that started
+    at phase 0 (y[m] uses x[(m+1)M - 1 - i], i < taps; decim.rs:221-228): (first input,
+    input count); the outputs are the zero-state dot products of the length-`taps`
+    windows starting every M inputs.  Needs (m+1)M >= taps."""
+    first = (m + 1) * M - taps
+    if first < 0:
+        raise ValueError("window starts before the first full delay line")
+    return first, (width - 1) * M + taps
+
+
+def check_gathered(big, expected, rng, width: int, lo: int, hi: int, windows: int = 2) -> float:
+    """Worst relative RMS error over `windows` random output windows [s, s + width),
+    lo <= s <= hi - width, of every row of a gathered [ranks, n] output (row r =
+    channel r), against expected(r, s, width)."""
+    import numpy as np
+    worst = 0.0
+    rows = big.shape[0]
+    for r in range(rows):
+        for _ in range(windows):
+            s = int(rng.integers(lo, hi - width + 1))
+            ref = np.asarray(expected(r, s, width), dtype=np.complex128)
+            got = big[r, s:s + width]
+            got = got.cpu().numpy() if hasattr(got, "cpu") else np.asarray(got)
+            got = np.asarray(got, dtype=np.complex128)
+            if got.shape != ref.shape:
+                return float("inf")
+            worst = max(worst, float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-300)))
+    return worst

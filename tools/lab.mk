@@ -19,5 +19,9 @@ tools/_build/lab/%.o: $(CSRC)/%.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
 	@mkdir -p tools/_build/lab
 	$(HIPCC) $(HIPFLAGS) -DSDSP_OLS_LAB -DSDSP_CHAN_LAB -DSDSP_IIR_LAB -DSDSP_PFB_LAB -c $< -o $@
 
+# the slot kernel's queue atomic is issued by one lane and its result is needed a segment later: no
+# wave-level atomic rewrite (it waits for the returned value at once)
+tools/_build/lab/kern_fir_ols_os.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+
 $(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_SRC)) $(PRODUCT_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^
