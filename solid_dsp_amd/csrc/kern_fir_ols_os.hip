@@ -299,7 +299,31 @@ __device__ __forceinline__ bool slot_barrier(unsigned* ctr, unsigned target) {
     return spin < kSpinLimit;
 }
 
-// ABL (lab builds only): 1 HBM traffic only (rows stored as loaded), 2 compute only (no loads, no stores)
+// segment loads the compiler does not track (ABL 3): it then places no waits for them, and the
+// one explicit wait lets the 16 younger stores of the previous segment stay in flight
+typedef unsigned u4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u4s rsrc_words(const void* base, unsigned bytes) {
+    const unsigned long long a = (unsigned long long)base;
+    return u4s{(unsigned)a, (unsigned)(a >> 32) & 0xffffu, bytes, (unsigned)kBufWord3};
+}
+__device__ __forceinline__ f2 ld_untracked(u4s rs, unsigned voff, unsigned soff) {
+    f2 r;
+    asm volatile("buffer_load_dwordx2 %0, %1, %2, %3 offen" : "=v"(r) : "v"(voff), "s"(rs), "s"(soff) : "memory");
+    return r;
+}
+// wait for every vector-memory operation but the 16 youngest (the segment's stores, or the
+// 16 dropped stores of the prologue); ties the loaded registers so nothing reads them earlier
+__device__ __forceinline__ void wait_loads16(f2 (&v)[16]) {
+    asm volatile("s_waitcnt vmcnt(16)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                   "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]),
+                   "+v"(v[15])
+                 :
+                 : "memory");
+}
+
+// ABL (lab builds only): 1 HBM traffic only (rows stored as loaded), 2 compute only (no loads, no stores),
+// 3 full kernel with untracked segment loads
 template <int SLOTS, int ABL = 0>
 __global__ void __launch_bounds__(256 * SLOTS, 1)
 fir_ols_slot_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
@@ -345,9 +369,11 @@ fir_ols_slot_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, con
         const bool any = k < cnt;
         const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + chan + (s0 + (any ? k : 0)) * V - 256 * h2),
                                                           (short)0, any ? 32768 : 0, kBufWord3);
+        const u4s rxw = rsrc_words(x + chan + (s0 + (any ? k : 0)) * V - 256 * h2, any ? 32768u : 0u);
 #pragma unroll
         for (int r = 0; r < 16; ++r)
             if constexpr (ABL == 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)k};
+            else if constexpr (ABL == 3) v[r] = ld_untracked(rxw, 8 * t, 2048 * r);
             else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
         // 16 dropped stores (empty descriptor): the loop is entered with 16 vector-memory operations younger
         // than the segment loads on every path, so the waits at the top of the loop let a previous
@@ -355,6 +381,7 @@ fir_ols_slot_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, con
         const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 0, kBufWord3);
 #pragma unroll
         for (int r = 0; r < 16; ++r) __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rz, 8 * t, 2048 * r, 0);
+        if constexpr (ABL == 3) wait_loads16(v);
     }
     for (long long it = 0; k < cnt; ++it) {  // k uniform over the slot
         const long long base = chan + (s0 + k) * V - 256 * h2;
@@ -431,9 +458,11 @@ fir_ols_slot_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, con
             const bool more = kn < cnt;
             const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + chan + (s0 + (more ? kn : k)) * V - 256 * h2),
                                                               (short)0, more ? 32768 : 0, kBufWord3);
+            const u4s rxw = rsrc_words(x + chan + (s0 + (more ? kn : k)) * V - 256 * h2, more ? 32768u : 0u);
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 if constexpr (ABL == 2) vn[r] = f2{1e-3f * t + r, 1e-9f * (float)kn};
+                else if constexpr (ABL == 3) vn[r] = ld_untracked(rxw, 8 * t, 2048 * r);
                 else vn[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
         }
 
@@ -451,6 +480,7 @@ fir_ols_slot_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, con
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[ABL == 1 ? r : kout(r)]), r >= h2 ? ry : rz,
                                                       8 * t, 2048 * r, 0);
         }
+        if constexpr (ABL == 3) wait_loads16(vn);
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = vn[r];
         k = kn;
@@ -527,6 +557,9 @@ hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n,
         const int abl = (g_lab_variant >> 4) & 3;
         if (slots == 4 && abl == 1)
             hipLaunchKernelGGL((fir_ols_slot_kernel<4, 1>), g2, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows, qp, g_lab_tok);
+        else if (slots == 4 && abl == 3)
+            hipLaunchKernelGGL((fir_ols_slot_kernel<4, 3>), g2, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
                                (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows, qp, g_lab_tok);
         else if (slots == 4 && abl == 2)
             hipLaunchKernelGGL((fir_ols_slot_kernel<4, 2>), g2, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,

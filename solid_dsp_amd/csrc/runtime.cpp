@@ -666,7 +666,7 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
     if (hst) return hst;
     h->host_valid = false;  // the input is device-resident: the host window is re-read when needed
     // work queued on another stream (the fence) reads or writes the history this launch uses
-    if (h->fence.pending) SDSP_TRY(hipStreamWaitEvent(s, h->fence.ev, 0), "order after queued work");
+    SDSP_TRY(h->fence.order_before(s), "order after queued work");
     const void* hist = h->d_hist[h->cur].p;
     if (h->M == 1) {
         const int algo = fir_resolve_algo(h, n);

@@ -117,6 +117,7 @@ struct DevBuf {
 // never raced by a host copy on the handle's own stream.
 struct StreamFence {
     hipEvent_t ev = nullptr;
+    hipStream_t stream = nullptr;  // where the pending marker was recorded
     bool pending = false;
     StreamFence() = default;
     StreamFence(const StreamFence&) = delete;
@@ -130,7 +131,15 @@ struct StreamFence {
             if (e != hipSuccess) return e;
         }
         pending = true;
+        stream = s;
         return hipEventRecord(ev, s);
+    }
+    // order work about to be queued on `s` after the pending marker; nothing to do on the
+    // marker's own stream (stream order), and the event is never waited on from the stream
+    // that re-records it
+    hipError_t order_before(hipStream_t s) {
+        if (!pending || s == stream) return hipSuccess;
+        return hipStreamWaitEvent(s, ev, 0);
     }
     hipError_t wait() {
         if (!pending) return hipSuccess;

@@ -633,24 +633,24 @@ def test_host_step_bit_parity(dt, cdt, sdt, L, M):
     c = f.clone()                   # the clone takes the host window
     per_sample(4)
     device_block(257)
-    g2, r2 = [], []
-    for k in range(6):  # the clone continues from the snapshot
-        g2.extend(c.execute(x[100 + k]))
-    o2 = O.fir(dt, h, s) if M == 1 else O.decim(dt, h, s, M)
-    f.set_state(st, ph)
     per_sample(3)
     host_block(2)
     assert len(got) == len(ref)
     assert bits_equal(np.array(got, dtype=sdt), np.array(ref, dtype=sdt)), (L, M)
-    # the clone's outputs equal the original's from the same state
+    g2 = []
+    for k in range(6):  # the clone continues from the snapshot
+        g2.extend(c.execute(x[100 + k]))
+    # a handle restored to the snapshot gives the clone's outputs
     f.set_state(st, ph)
     g3 = []
     for k in range(6):
         g3.extend(f.execute(x[100 + k]))
     assert bits_equal(np.array(g2, dtype=sdt), np.array(g3, dtype=sdt))
-    f.reset()
-    o.reset()
+    f.reset()  # a zeroed delay line and phase: a fresh restatement (its FIR objects have no reset)
+    o = O.fir(dt, h, s) if M == 1 else O.decim(dt, h, s, M)
     per_sample(7)
+    device_block(300)
+    per_sample(2)
     assert bits_equal(np.array(got, dtype=sdt), np.array(ref, dtype=sdt))
     torch.cuda.synchronize()
 
