@@ -94,7 +94,8 @@ __device__ __forceinline__ unsigned int* cu_slot() {
 // (ablation: outputs dropped); 4 HBM traffic only (ablation: no transform);
 // 8/16/24: at most 1/2/3 workgroups per CU with segment loads in flight (a
 // per-CU ticket taken with vector atomics before the loads, returned once P1
-// has consumed them); 32: high wave priority while issuing loads and stores.
+// has consumed them); 32: high wave priority while issuing loads and stores; 128:
+// plain (not nontemporal) stores.
 template <int VAR>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -144,7 +145,9 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     if constexpr (VAR & 4) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-            if (r >= h2) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[r]), ry, 8 * t, 2048 * r, 0);
+            if (r >= h2)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[r]), ry, 8 * t, 2048 * r,
+                                                      (VAR & 128) ? 0 : 2);
 #ifdef SDSP_OLS_LAB
         if constexpr (kLim != 0) {
             __syncthreads();
@@ -235,9 +238,12 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
 #ifdef SDSP_OLS_LAB
     if constexpr (VAR & 32) __builtin_amdgcn_s_setprio(3);
 #endif
+    // nontemporal stores (3.14 -> 3.08 ms on cfg2, in-process A/B; lab bit 128: plain stores)
+    constexpr int kStAux = (VAR & 128) ? 0 : 2;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-        if (r >= h2) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, 0);
+        if (r >= h2)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, kStAux);
 }
 
 #ifdef SDSP_OLS_LAB  // lab only: measured slower than the one-shot kernel
@@ -537,7 +543,7 @@ extern "C" __attribute__((visibility("default"))) int sdsp_lab_hwid_probe(unsign
     hipLaunchKernelGGL(ols_hwid_probe_kernel, dim3(blocks), dim3(64), 40000, 0, d_out);
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
-#define SDSP_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(8) X(16) X(24) X(12) X(20) X(28) X(32) X(36) X(48) X(80) X(88) X(84) X(92)
+#define SDSP_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(8) X(16) X(24) X(12) X(20) X(28) X(32) X(36) X(48) X(80) X(88) X(84) X(92) X(128) X(132)
 #endif
 
 hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,

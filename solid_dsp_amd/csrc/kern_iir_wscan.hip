@@ -19,7 +19,8 @@
 //      are multiplied;
 //   4. outputs are corrected instead of rerun:  y[i] = y0[i] + Cr[i] . I_l,
 //      Cr[i] = c A^i (the output response to the state, precomputed on the
-//      host in f64), then leave with coalesced nontemporal 16-byte stores.
+//      host in f64, read as wave-uniform scalar loads), then leave with
+//      coalesced nontemporal 16-byte stores.
 // A wave's first tile starts `wc` chunks before its segment: those lanes run
 // the preceding input as warm-up (outputs dropped), which makes the carried-in
 // state exact to ||A^(wc B)|| < 1e-9 (f32) / 1e-17 (f64), the criterion the
@@ -179,9 +180,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     char* slab = lds_raw + wave * kSlabBytes;
     char* row = slab + lane * kRowBytes;
     C* sP = reinterpret_cast<C*>(lds_raw + kWsWaves * kSlabBytes);
-    C* sCr = sP + 6 * D * D;
     for (int i = threadIdx.x; i < 6 * D * D; i += kWsThreads) sP[i] = P[i];
-    for (int i = threadIdx.x; i < B * D; i += kWsThreads) sCr[i] = Cr[i];
     __syncthreads();
 
     const int ch = blockIdx.y;
@@ -343,7 +342,9 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 __builtin_memcpy(e, &val, 16);
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
-                    const C* cr = sCr + (o * E + i) * D;
+                    // Cr row of sample o E + i: wave-uniform, read through the scalar cache into
+                    // SGPR operands (an LDS broadcast read costs a full ds_read_b128 per 4 values)
+                    const C* cr = Cr + (o * E + i) * D;
 #pragma unroll
                     for (int d = 0; d < D; ++d) e[i] = fmac_(e[i], cr[d], init[d]);
                 }
@@ -813,7 +814,7 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     // 16-byte vector path: aligned bases and channel strides
     const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
                         (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
-    const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * D * D + B * D);
+    const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * D * D);
     const long long j0 = a.Md > 1 ? (long long)((a.Md - 1 - a.phase) % a.Md) : 0;  // first emitting domain index
     const long long ny = a.Md > 1 ? (long long)a.nout : nd;
     if (exact) {

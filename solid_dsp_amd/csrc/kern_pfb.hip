@@ -150,7 +150,7 @@ interp_tile_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C*
             a0 = mac<EXACT>(a0, c0[i], s);
             a1 = mac<EXACT>(a1, c1[i], s);
         }
-        if (jg + r < n) *reinterpret_cast<Pair<I>*>(yo + (long long)r * M) = Pair<I>{a0, a1};
+        if (jg + r < n) store_nt(reinterpret_cast<Pair<I>*>(yo + (long long)r * M), Pair<I>{a0, a1});
     }
 }
 

@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(256) nco_mix_kernel(const cpx<T>* __restrict__
         if (v < nv) {
 #pragma unroll
             for (int k = 0; k < V; ++k) r[u].s[k] = nco_one<T, DOWN>(lut, r[u].s[k], v * V + k, theta0, dtheta);
-            yv[v] = r[u];
+            store_nt(yv + v, r[u]);
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * V) {  // ragged tail (c32, odd n)

@@ -73,4 +73,24 @@ __device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned nb) {
     return b < 8 * q ? (b % 8) * q + b / 8 : b;
 }
 
+// A streaming store that bypasses the caches' normal retention (nontemporal):
+// T is copied out as 16-byte (or 8-byte) vector stores.  Outputs that no kernel
+// of the same call reads again (cfg2 OLS: 3.14 -> 3.08 ms, in-process A/B).
+template <typename T> __device__ __forceinline__ void store_nt(T* p, const T& v) {
+    static_assert(sizeof(T) % 8 == 0, "store_nt: 8-byte multiples");
+    if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        u4 w[sizeof(T) / 16];
+        __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(T) / 16; ++i) __builtin_nontemporal_store(w[i], reinterpret_cast<u4*>(p) + i);
+    } else {
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        u2 w[sizeof(T) / 8];
+        __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(T) / 8; ++i) __builtin_nontemporal_store(w[i], reinterpret_cast<u2*>(p) + i);
+    }
+}
+
 }  // namespace sdsp

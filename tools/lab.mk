@@ -23,5 +23,7 @@ tools/_build/lab/%.o: $(CSRC)/%.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
 # wave-level atomic rewrite (it waits for the returned value at once)
 tools/_build/lab/kern_fir_ols_os.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 
+tools/_build/lab/kern_iir_wscan.o: HIPFLAGS += -fno-slp-vectorize
+
 $(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_SRC)) $(PRODUCT_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^
