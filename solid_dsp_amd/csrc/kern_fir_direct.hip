@@ -123,7 +123,7 @@ fir_direct_kernel(const I* __restrict__ x, const I* __restrict__ hist, const C* 
     const long long o = t0 + b;
     if (o + R <= n) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) y[o + r] = mul_(acc[r], scale);
+        for (int r = 0; r < R; ++r) y[o + r] = mul_(acc[r], scale);  // plain: nontemporal +5 %
     } else {
 #pragma unroll
         for (int r = 0; r < R; ++r)

@@ -163,7 +163,7 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
             for (int j = 0; j < 16; ++j) {
                 const int v = lane + 64 * j;
                 if ((v >> 4) < nch)
-                    *reinterpret_cast<v4u*>(y + vaddr(k0, v)) =
+                    *reinterpret_cast<v4u*>(y + vaddr(k0, v)) =  // plain: nontemporal +1.7 % (cfg11)
                         *reinterpret_cast<const v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16);
             }
         } else {

@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__
     for (int r = 0; r < kR; ++r) p[pad8(kR * t + r)] = acc[r];
     __syncthreads();
     for (int s = t; s < kOut; s += kTile)
-        if (n0 + s < n) y[n0 + s] = p[pad8(s)];
+        if (n0 + s < n) store_nt(y + n0 + s, p[pad8(s)]);
 }
 
 // execute() on the current window (no push): the output for the newest history sample
@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(64, 4) agc_kernel(const AgcSample<CPLX>* __res
 #pragma unroll
         for (int k = 0; k < kAgcS; ++k) {
             const int e = t + 64 * k, c = e / kAgcS, j = e % kAgcS;
-            if (j < cnt && ch0 + c < channels) y[(ch0 + c) * n + i0 + j] = buf[c * (kAgcS + 1) + j];
+            if (j < cnt && ch0 + c < channels) y[(ch0 + c) * n + i0 + j] = buf[c * (kAgcS + 1) + j];  // plain: nontemporal +7 %
         }
         __syncthreads();
     }

@@ -74,11 +74,16 @@ __device__ __forceinline__ unsigned xcd_order(unsigned b, unsigned nb) {
 }
 
 // A streaming store that bypasses the caches' normal retention (nontemporal):
-// T is copied out as 16-byte (or 8-byte) vector stores.  Outputs that no kernel
+// T is copied out as 16-, 8- or 4-byte stores (by its size and alignment).  Outputs that no kernel
 // of the same call reads again (cfg2 OLS: 3.14 -> 3.08 ms, in-process A/B).
 template <typename T> __device__ __forceinline__ void store_nt(T* p, const T& v) {
-    static_assert(sizeof(T) % 8 == 0, "store_nt: 8-byte multiples");
-    if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
+    static_assert(sizeof(T) % 4 == 0, "store_nt: 4-byte multiples");
+    if constexpr (sizeof(T) % 8 != 0 || alignof(T) < 8) {
+        unsigned w[sizeof(T) / 4];
+        __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(T) / 4; ++i) __builtin_nontemporal_store(w[i], reinterpret_cast<unsigned*>(p) + i);
+    } else if constexpr (sizeof(T) % 16 == 0 && alignof(T) >= 16) {
         typedef unsigned u4 __attribute__((ext_vector_type(4)));
         u4 w[sizeof(T) / 16];
         __builtin_memcpy(w, &v, sizeof(T));
