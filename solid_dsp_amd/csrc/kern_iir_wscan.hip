@@ -885,11 +885,12 @@ extern "C" __attribute__((visibility("default"))) int sdsp_lab_set_iir_ablation(
 }
 #endif
 
-size_t iir_wscan_waves(int dtype, const IirArgs& a) {
+size_t iir_wscan_waves(int dtype, const IirArgs& a, int* tpw_out) {
     const int B = iir_wscan_chunk(dtype, a.ws_variant == 1 ? 1 : 0);
     if (B == 0) return 0;
     const long long nch = ((long long)a.n * a.Mi + B - 1) / B;
     const int tpw = a.ws_variant == 1 ? wscan_tpw<128>(nch) : wscan_tpw<256>(nch);
+    if (tpw_out) *tpw_out = tpw;
     const long long segc = (long long)tpw * 64 - a.wc;
     return (size_t)((nch + segc - 1) / segc);
 }

@@ -39,6 +39,7 @@ struct Group {
         bool exact = false;    // wc == 0 but bounded: exact inter-wave carries (Phi)
         DevBuf d_P, d_Cr;      // [6][2c][2c], [B][2c] output response to the state
         DevBuf d_Phi;          // exact carries: [8][2c][2c] A^(64 B t), t = 1..8
+        long long phi_wmax[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // per tpw: waves the carry chain admits
     } ws[5];
 };
 
@@ -323,6 +324,33 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
     IIR_TRY(dCr->ensure(Cr.size()), "alloc Cr");
     IIR_TRY(hipMemcpy(dCr->p, Cr.data(), Cr.size(), hipMemcpyHostToDevice), "copy Cr");
     return SDSP_OK;
+}
+
+// Exact inter-wave carries (wc == 0) run through Phi = A^(64 B tpw) and, in the
+// one-block carry kernel, Phi^R (R = ceil(W / 256), by repeated squaring in the Coef
+// type) and 256 chained applications of it: the carried state is multiplied by
+// powers of Phi up to Phi^W.  The plan-time probe covers chunk carries over 2^14
+// samples only, so each call also bounds the powers it will use: ||Phi^(2^j)||_inf <=
+// 1e6 for every 2^j < 2 W (checked in f64, once per tpw, cached as the largest W
+// admitted).  A marginally stable system whose powers grow (a double pole at z = 1:
+// ||A^m|| ~ m) is admitted for short calls and runs the reference-order recurrence
+// for long ones; bounded powers (a single pole at z = 1, poles on the unit circle)
+// admit every length.
+bool exact_carry_bounded(const sdsp_iir* h, Group& g, int wv, size_t waves, int tpw) {
+    if (tpw < 1 || tpw > 8) return false;
+    long long& wmax = g.ws[wv].phi_wmax[tpw];
+    if (wmax < 0) {
+        const int D = group_dim(h, g), B = iir_wscan_chunk(h->dtype, wv);
+        Mat P = matpow(matpow(sys_A(h, g), B, D), 64LL * tpw, D);
+        wmax = 0;
+        for (int j = 0; j < 48; ++j) {
+            const double nrm = norm_inf(P, D);
+            if (!std::isfinite(nrm) || nrm > 1e6) break;
+            wmax = (2LL << j) - 1;  // every power up to 2^(j+1) - 1 is a product of checked squares' neighbours
+            P = matmul(P, P, D);
+        }
+    }
+    return (long long)waves <= wmax;
 }
 
 int plan_groups(sdsp_iir* h) {
@@ -623,28 +651,33 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
         IirArgs a{d_in, d_out, h->d_coefs.p, nullptr, st_in, st_out, n, nout, h->channels, 0, h->nb, h->na, h->cap,
                   Mi, Md, h->phase, false, 0};
         const bool rc = Mi != 1 || Md != 1;
+        bool scanned = false;
         if (!h->groups.empty() && group_scan(h, h->groups[0], nd, rc)) {  // dense-system wave scan
-            const Group& gr = h->groups[0];
-            a.coefs = h->d_coefs_nrm.p;
-            a.algo_scan = true;
-            a.P = gr.ws[0].d_P.p;
-            a.Cr = gr.ws[0].d_Cr.p;
-            a.wc = gr.ws[0].wc;
-            a.ws_variant = 0;
-            if (a.wc == 0) {
-                a.Phi = gr.ws[0].d_Phi.p;
-                const size_t W = iir_wscan_waves(h->dtype, a);
-                const size_t bytes = h->channels * W * (size_t)(h->cap - 1) * sbytes;
-                IIR_TRY(h->d_carry[0].ensure(bytes), "iir carry scratch");
-                IIR_TRY(h->d_carry[1].ensure(bytes), "iir carry scratch");
-                a.G = h->d_carry[0].p;
-                a.Cin = h->d_carry[1].p;
-                a.scratch_waves = W;
+            Group& gr = h->groups[0];
+            IirArgs b = a;
+            b.coefs = h->d_coefs_nrm.p;
+            b.algo_scan = true;
+            b.P = gr.ws[0].d_P.p;
+            b.Cr = gr.ws[0].d_Cr.p;
+            b.wc = gr.ws[0].wc;
+            b.ws_variant = 0;
+            int tpw = 0;
+            const size_t W = iir_wscan_waves(h->dtype, b, &tpw);
+            if (b.wc > 0 || exact_carry_bounded(h, gr, 0, W, tpw)) {  // else the reference-order recurrence
+                if (b.wc == 0) {
+                    b.Phi = gr.ws[0].d_Phi.p;
+                    const size_t bytes = h->channels * W * (size_t)(h->cap - 1) * sbytes;
+                    IIR_TRY(h->d_carry[0].ensure(bytes), "iir carry scratch");
+                    IIR_TRY(h->d_carry[1].ensure(bytes), "iir carry scratch");
+                    b.G = h->d_carry[0].p;
+                    b.Cin = h->d_carry[1].p;
+                    b.scratch_waves = W;
+                }
+                IIR_TRY(launch_iir_wscan(h->dtype, b, s), "iir normal wave scan");
+                scanned = true;
             }
-            IIR_TRY(launch_iir_wscan(h->dtype, a, s), "iir normal wave scan");
-        } else {
-            IIR_TRY(launch_iir(h->dtype, a, s), "iir normal");
         }
+        if (!scanned) IIR_TRY(launch_iir(h->dtype, a, s), "iir normal");
     } else {
         const size_t ng = h->groups.size();
         if (ng > 1) {
@@ -654,7 +687,7 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
         size_t soff = 0;
         const void* src = d_in;
         for (size_t gi = 0; gi < ng; ++gi) {
-            const Group& gr = h->groups[gi];
+            Group& gr = h->groups[gi];
             const bool first = gi == 0, last = gi + 1 == ng;
             void* dst = last ? d_out : h->d_tmp[gi & 1].p;
             const size_t n_g = first ? n : nd;
@@ -663,7 +696,16 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
                       st_in + soff, st_out + soff, n_g, last ? nout : nd, h->channels, gr.count, 0, 0, 0,
                       first ? Mi : 1, last ? Md : 1, last ? h->phase : 0, group_scan(h, gr, nd, rc), gr.wc};
             const int wv = group_wscan(h, gr, rc);
-            if (a.algo_scan && wv >= 0) {
+            bool wave_scan = a.algo_scan && wv >= 0;
+            if (wave_scan && gr.ws[wv].wc == 0) {  // exact carries: the powers of Phi this call uses stay bounded
+                IirArgs b = a;
+                b.wc = 0;
+                b.ws_variant = wv;
+                int tpw = 0;
+                const size_t W = iir_wscan_waves(h->dtype, b, &tpw);
+                wave_scan = exact_carry_bounded(h, gr, wv, W, tpw);
+            }
+            if (wave_scan) {
                 a.P = gr.ws[wv].d_P.p;
                 a.Cr = gr.ws[wv].d_Cr.p;
                 a.wc = gr.ws[wv].wc;
@@ -679,8 +721,8 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
                     a.scratch_waves = W;
                 }
                 IIR_TRY(launch_iir_wscan(h->dtype, a, s), "iir sos wave scan");
-            } else if (a.algo_scan && gr.wc == 0) {  // block scan needs the decaying response
-                a.algo_scan = false;
+            } else if (a.algo_scan && (gr.wc == 0 || wv >= 0)) {  // block scan needs the decaying response;
+                a.algo_scan = false;                             // an unbounded carry chain runs serial
                 IIR_TRY(launch_iir(h->dtype, a, s), "iir sos");
             } else {
                 IIR_TRY(launch_iir(h->dtype, a, s), "iir sos");

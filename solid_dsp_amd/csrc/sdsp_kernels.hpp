@@ -109,7 +109,7 @@ struct IirArgs {
     size_t scratch_waves = 0;  // capacity of G / Cin per channel
 };
 // waves the exact-carry wave scan launches for this call (sizes G / Cin)
-size_t iir_wscan_waves(int dtype, const IirArgs& a);
+size_t iir_wscan_waves(int dtype, const IirArgs& a, int* tpw = nullptr);  // waves (and tiles per wave) of one call
 hipError_t launch_iir(int dtype, const IirArgs& a, hipStream_t s);
 int iir_scan_chunk(int dtype);  // samples per lane chunk of the scan kernel
 // wave-level scan (kern_iir_wscan.hip): SOS cascades, with rate changes; wc <= 32

@@ -375,6 +375,48 @@ def test_exact_carry_scan_nondecaying(dt, cdt, sdt, tol, kind):
     assert len(yd) == len(refd) and rel_rms(yd, refd) <= tol
 
 
+@pytest.mark.parametrize("dt,cdt,sdt,tol", [(O.RR64, np.float64, np.float64, 1e-12),
+                                            (O.RR32, np.float32, np.float32, 2e-5)])
+def test_exact_carry_scan_long_call(dt, cdt, sdt, tol):
+    """the exact-carry chain at bench-like lengths -- 2^24 + 3 samples in one call
+    (W = 512 waves, Phi^R with R = 2 in the carry kernel) through the integrator cascade
+    (a pole at z = 1 behind a decaying section), against the f64 reference-order loop"""
+    ff = np.array([1.0, 0.0, 0.0, 0.2, 0.2, 0.0]).astype(cdt)
+    fb = np.array([1.0, -1.0, 0.0, 1.0, -0.6, 0.0]).astype(cdt)
+    rng = np.random.default_rng(24)
+    n = (1 << 24) + 3
+    x = rand(rng, n, sdt)
+    f = IIRFilter(ff, fb, SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    assert f.wscan_mode() == 2
+    y = f.execute_block(x)
+    ref = O.iir(O.RR64, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER).execute_block(x.astype(np.float64))
+    if cdt == np.float32:
+        tol = max(tol, 10 * rel_rms(O.iir(dt, ff, fb, O.SECOND_ORDER).execute_block(x), ref))
+    assert rel_rms(y, ref) <= tol, (rel_rms(y, ref), tol)
+    z = rand(rng, 4096, sdt)  # the exact final state: one more call continues the stream
+    ref2 = O.iir(O.RR64, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER).execute_block(
+        np.concatenate([x, z]).astype(np.float64))[n:]
+    assert rel_rms(f.execute_block(z), ref2) <= max(tol, 1e-9)
+
+
+def test_exact_carry_growing_powers_run_serial():
+    """a double pole at z = 1 (||A^m|| ~ m) passes the short host probe, but the powers
+    of Phi a long call would chain grow past the bound: that call runs the reference-order
+    recurrence -- bit-identical to the reference -- while a short call may still scan"""
+    ff = np.array([1.0, 0.0, 0.0])
+    fb = np.array([1.0, -2.0, 1.0])
+    rng = np.random.default_rng(5)
+    n = 1 << 22
+    x = rand(rng, n, np.float64)
+    f = IIRFilter(ff, fb, SO, sample_dtype=np.float64, algo=sd.ALGO_FMA)
+    y = f.execute_block(x)
+    assert bits_equal(y, O.iir(O.RR64, ff, fb, O.SECOND_ORDER).execute_block(x))
+    g = IIRFilter(ff, fb, SO, sample_dtype=np.float64, algo=sd.ALGO_FMA)
+    xs = x[: (1 << 15) + 7]
+    ref = O.iir(O.RR64, ff, fb, O.SECOND_ORDER).execute_block(xs)
+    assert rel_rms(g.execute_block(xs), ref) <= 1e-9
+
+
 @pytest.mark.parametrize("dt,cdt,sdt,tol", [(O.RR32, np.float32, np.float32, 1e-5), (O.RC32, np.float32, np.complex64, 1e-5),
                                             (O.RR64, np.float64, np.float64, 1e-12), (O.RC64, np.float64, np.complex128, 1e-12)])
 @pytest.mark.parametrize("order", [2, 4, 8])
