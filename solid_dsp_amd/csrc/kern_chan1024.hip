@@ -520,6 +520,107 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
     }
 }
 
+// Persistent, software-pipelined form of the pass above (the default for
+// TPB = 16): grid = one 1024-thread workgroup per CU, workgroup b runs groups b,
+// b + G, b + 2G, ... of 16 transforms.  The loads of the next group are issued
+// into registers BEFORE the current group's FFT and stores, so each CU's HBM
+// queue never drains while it transforms (the one-shot kernel alternated: load,
+// barrier, FFT, barrier, store, with one 141 KB workgroup per CU and nothing else
+// resident).  At step k the chip's workgroups run the neighbouring groups
+// kG .. kG + G - 1: on the strided (column) side the rows they read are 32 KB
+// contiguous runs.  Same arithmetic, element order and twiddles as
+// fft1024_pass_kernel<INV, TW, 16> (bit-identical).
+#ifndef SDSP_FFT_PIPE_PRE
+#define SDSP_FFT_PIPE_PRE 16
+#endif
+template <bool INV, bool TW, bool CFAST, bool OFAST>
+__global__ void __launch_bounds__(1024)
+fft1024_pipe_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __restrict__ tw,
+                    const cf* __restrict__ twx, long long count, long long G, long long S0, long long S1,
+                    long long Si, long long T1, long long So) {
+    constexpr int TPB = 16, kT = 1024, kLog = 4;
+    constexpr int kPre = SDSP_FFT_PIPE_PRE;  // next-group loads issued before the FFT (the rest after it)
+    __shared__ cf stw[kM];
+    __shared__ cf sbuf[TPB * kPassBuf];
+    __shared__ cf ktab[TW ? TPB * 16 : 1];
+    const int t = threadIdx.x, L = t & 63, w = t >> 6;
+    const long long ngroups = count / TPB;
+    stw[t] = tw[t];
+    auto twx_at = [&](long long m) -> cf {
+        const unsigned u = (unsigned)(m & ((1 << 20) - 1));
+        return cmul(twx[1024 + (u >> 10)], twx[u & 1023]);
+    };
+    constexpr bool cfast = CFAST, ofast = OFAST;  // compile-time: LDS offsets fold into immediates
+    // group -> (input base, output base, first column g0)
+    auto bases = [&](long long grp, long long& ib, long long& ob, long long& g0) {
+        const long long t0 = grp * TPB;
+        g0 = t0 % G;
+        ib = (t0 / G) * S0 + g0 * S1;
+        ob = (t0 / G) * S0 + g0 * T1;
+    };
+    // element k of thread t sits at lane offset + k * (scalar stride): buffer loads and
+    // stores with one offset VGPR (64-bit addresses per element spill the pipeline's
+    // registers).  cfast: c = t & 15, i = (t >> 4) + 64 k; else c = k, i = t.
+    const unsigned in_lane = (unsigned)(cfast ? ((t & 15) + (long long)(t >> 4) * Si) : (long long)t * Si) * 8u;
+    const unsigned in_k = (unsigned)(cfast ? 64 * Si : S1) * 8u;
+    const unsigned out_lane = (unsigned)(ofast ? ((t & 15) + (long long)(t >> 4) * So) : (long long)t * So) * 8u;
+    const unsigned out_k = (unsigned)(ofast ? 64 * So : T1) * 8u;
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    cf v[16];
+    auto load = [&](long long grp, int k0, int k1) {
+        long long ib, ob, g0;
+        bases(grp, ib, ob, g0);
+        const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + ib), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int k = k0; k < k1; ++k)
+            v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, 0));
+    };
+    long long grp = blockIdx.x;
+    if (grp >= ngroups) return;  // uniform
+    load(grp, 0, 16);
+    for (;;) {
+        // stage the group's columns (waits for its loads: the previous stores may stay in flight)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int e = t + kT * k;
+            const int c = cfast ? (e & (TPB - 1)) : (e >> 10), i = cfast ? (e >> kLog) : (e & 1023);
+            sbuf[c * kPassBuf + i] = INV ? cf{v[k].re, -v[k].im} : v[k];
+        }
+        long long ib, ob, g0;
+        bases(grp, ib, ob, g0);
+        cf tbase = cf{1.0f, 0.0f};
+        if constexpr (TW) {
+            if (t < TPB * 16) ktab[t] = twx_at(64 * (g0 + (t >> 4)) * (long long)(t & 15));
+            if (ofast) tbase = twx_at((g0 + (t & (TPB - 1))) * (long long)(t >> kLog));
+        }
+        __syncthreads();
+        // the next group's loads: half in flight across this group's FFT, half across its
+        // stores (all sixteen held through the FFT spill registers at 1024 threads)
+        const long long nxt = grp + gridDim.x;
+        if (nxt < ngroups) load(nxt, 0, kPre);
+        fft1024_wave_lds(sbuf + w * kPassBuf, stw, L);
+        __syncthreads();
+        if (nxt < ngroups) load(nxt, kPre, 16);
+        const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ob), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int e = t + kT * k;
+            const int c = ofast ? (e & (TPB - 1)) : (e >> 10), i = ofast ? (e >> kLog) : (e & 1023);
+            cf r = sbuf[c * kPassBuf + i];
+            if (INV) r.im = -r.im;
+            if constexpr (TW) {
+                cf wv = ofast ? cmul(tbase, ktab[c * 16 + k]) : twx_at((g0 + c) * (long long)i);
+                if (INV) wv.im = -wv.im;
+                r = cmul(r, wv);
+            }
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, r), ry, out_lane, k * out_k, 0);
+        }
+        if (nxt >= ngroups) break;
+        grp = nxt;
+        __syncthreads();  // every read of sbuf / ktab done before the next group is staged
+    }
+}
+
 }  // namespace
 
 #ifdef SDSP_CHAN_LAB
@@ -580,15 +681,41 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
 
 // four-step pass of L = 1024 on the wave FFT; false = not applicable
 bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
+    // SDSP_FFT_WAVE1024: 16 (default) the pipelined persistent kernel, 1 the one-shot kernel
+    // with 16 transforms per workgroup, 8 one-shot with 8, 0 the generic Stockham pass
     static const int tpb = [] {
         const char* e = std::getenv("SDSP_FFT_WAVE1024");
         const int v = e ? std::atoi(e) : 16;
-        return v == 0 || v == 8 ? v : 16;
+        return v == 0 || v == 8 || v == 1 ? v : 16;
     }();
-    if (tpb == 0 || p.L != 1024 || p.count % tpb != 0 || p.G % tpb != 0) return false;
+    if (tpb == 0 || p.L != 1024 || p.count % 16 != 0 || p.G % 16 != 0) return false;
     if (!(p.S1 == 1 || p.Si == 1) || !(p.T1 == 1 || p.So == 1)) return false;
     if (p.Ntw && (p.Ntw != (1LL << 20) || !p.twx)) return false;
-    dim3 grid((unsigned)(p.count / tpb));
+    if (tpb == 16) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const long long groups = p.count / 16;
+        const dim3 g2((unsigned)(groups < cus ? groups : cus));
+        const bool cf_ = p.S1 == 1, of_ = p.T1 == 1;
+#define SDSP_PIPE4(INV, TW, C, O)                                                                                 \
+    hipLaunchKernelGGL((fft1024_pipe_kernel<INV, TW, C, O>), g2, dim3(1024), 0, s, (const cf*)p.x, (cf*)p.y,      \
+                       (const cf*)p.tw, (const cf*)p.twx, p.count, p.G, p.S0, p.S1, p.Si, p.T1, p.So)
+#define SDSP_PIPE(INV, TW)                                                                         \
+    do {                                                                                           \
+        if (cf_) { if (of_) SDSP_PIPE4(INV, TW, true, true); else SDSP_PIPE4(INV, TW, true, false); }   \
+        else { if (of_) SDSP_PIPE4(INV, TW, false, true); else SDSP_PIPE4(INV, TW, false, false); } \
+    } while (0)
+        if (p.inverse) {
+            if (p.Ntw) SDSP_PIPE(true, true); else SDSP_PIPE(true, false);
+        } else {
+            if (p.Ntw) SDSP_PIPE(false, true); else SDSP_PIPE(false, false);
+        }
+#undef SDSP_PIPE
+#undef SDSP_PIPE4
+        *err = hipGetLastError();
+        return true;
+    }
+    dim3 grid((unsigned)(p.count / (tpb == 1 ? 16 : tpb)));
 #define SDSP_P1024(INV, TW, TPB)                                                                                  \
     hipLaunchKernelGGL((fft1024_pass_kernel<INV, TW, TPB>), grid, dim3(64 * TPB), 0, s, (const cf*)p.x, (cf*)p.y, \
                        (const cf*)p.tw, (const cf*)p.twx, p.count, p.G, p.S0, p.S1, p.Si, p.T1, p.So)
@@ -598,7 +725,7 @@ bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
     } else {                                                                              \
         if (p.Ntw) SDSP_P1024(false, true, TPB); else SDSP_P1024(false, false, TPB);      \
     }
-    if (tpb == 16) {
+    if (tpb == 1) {
         SDSP_P1024_T(16)
     } else {
         SDSP_P1024_T(8)
