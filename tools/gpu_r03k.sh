@@ -1,5 +1,5 @@
 #!/bin/bash
-# r03k: FFT parity with the pipelined pass kernel, then cfg8 pipe vs one-shot (SDSP_FFT_WAVE1024=1)
+# r03k: FFT parity with the pipelined pass kernel (blocked four-step intermediate), then cfg8 pipe vs one-shot (SDSP_FFT_WAVE1024=1)
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_fft.py tests/test_gpu_golden.py -m gpu -x -q --timeout 120 \
