@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--no-gather", action="store_true", help="skip the final RCCL gather of every rank's output")
     p.add_argument("--no-dropin", action="store_true", help="config 2: skip the drop-in cost figures")
+    p.add_argument("--shard", default="channel", choices=["channel", "time"],
+                   help="configs 2 and 4: independent channels per rank (default), or one long stream "
+                        "time-sharded (rank r filters inputs [r n, (r+1) n) after an (L-1)-input halo)")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU-only rehearsal of the rank launch, timing and gather over gloo (no GPU)")
     return p.parse_args()
@@ -134,7 +137,37 @@ def timed_cpu(run_chunk, label, samples, chunk, cores=1):
 
 
 # --------------------------------------------------------------------------- workloads
-class Cfg2FIR:
+class StreamShard:
+    """Configs 2 and 4: a stream per rank, or one stream time-sharded over the ranks."""
+
+    def time_sharded(self, args, rank, torch, sd, P_halo, m_per_in=1):
+        """input of this rank: its own channel (channel = rank), or with --shard time
+        segment `rank` of ONE stream (channel 0) plus the halo of inputs before it
+        (parallel.time_segment); the halo block is filtered first in every step and its
+        outputs dropped, so the segment's outputs are the single stream's"""
+        from solid_dsp_amd import parallel as P
+        cs = torch.cuda.current_stream().cuda_stream
+        self.shard = getattr(args, "shard", "channel")
+        self.halo = 0
+        if self.shard != "time":
+            sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n, cs)
+            return
+        first, self.halo = P.time_segment(self.n, rank, P_halo(P))
+        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, 0, 2 * rank * self.n, 2 * self.n, cs)
+        self.d_halo = torch.empty(max(self.halo, 1), dtype=torch.complex64, device="cuda")
+        self.d_halo_out = torch.empty(max(self.halo // m_per_in, 1), dtype=torch.complex64, device="cuda")
+        if self.halo:
+            sd.lib().sdsp_synth_f32_device(self.d_halo.data_ptr(), SEED, 0, 2 * first, 2 * self.halo, cs)
+        self.parallelism = ("one stream (channel 0) time-sharded: rank r filters inputs [r n, (r+1) n) after a "
+                            f"{P_halo(P)}-input halo, no exchange")
+
+    def step(self, stream):
+        if self.halo:  # time-sharded: the delay line from the segment's halo
+            self.f.execute_block_device(self.d_halo, self.halo, self.d_halo_out, stream)
+        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+
+
+class Cfg2FIR(StreamShard):
     """256-tap crcf FIR, firdes_kaiser(256, 0.1, 80) taps rounded to f32, scale 0.2."""
     metric = "Msamples/sec 256-tap complex FIR @1/2/4/8 GPU; % HBM roofline"
     taps = 256
@@ -151,8 +184,7 @@ class Cfg2FIR:
         self.make = lambda: FIRFilter(self.h, np.float32(0.2), sample_dtype=np.complex64, device=dev, algo=self.algo)
         self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
         self.d_out = torch.empty(self.n, dtype=torch.complex64, device="cuda")
-        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
-                                       torch.cuda.current_stream().cuda_stream)
+        self.time_sharded(args, rank, torch, sd, P_halo=lambda P: P.fir_halo(self.taps))
         self.samples_per_step = self.n
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (f32 taps x complex-f32 samples, f32 accumulate)"
@@ -162,9 +194,6 @@ class Cfg2FIR:
                        "fma": "fir_direct_kernel<FMA>"}[args.algo]
         self.workload = (f"cfg2: 256-tap crcf FIR, firdes_kaiser(256, 0.1, 80), scale 0.2, 2^{args.log2n} samples "
                          "per channel, device resident")
-
-    def step(self, stream):
-        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
 
     def parity(self, stream, rng, windows=4, width=4096):
         """random output windows recomputed on the CPU (f64 restatement) from the L-1 preceding inputs"""
@@ -194,8 +223,11 @@ class Cfg2FIR:
         return O.fir(O.RC64, np.asarray(h, np.float64), 0.2).execute_block(xs)[drop:]
 
     def check_gathered(self, big, rng, width=4096):
-        """every rank's gathered output (channel = rank): two random windows each"""
+        """every rank's gathered output (channel = rank): two random windows each; time-sharded:
+        windows of the one stream inside every segment and across every segment boundary"""
         from solid_dsp_amd import parallel as P
+        if self.shard == "time":
+            return P.check_time_sharded(big, lambda g, w: Cfg2FIR.expected(self.h, 0, g, w), rng, width, self.taps)
         return P.check_gathered(big, lambda r, s, w: Cfg2FIR.expected(self.h, r, s, w), rng, width, self.taps,
                                 self.n)
 
@@ -256,7 +288,7 @@ class Cfg3IIR:
                          CPU_CHUNK)
 
 
-class Cfg4Decim:
+class Cfg4Decim(StreamShard):
     """M=32 decimator, firdes_kaiser(256, 1/64, 80) rounded to f32, scale 1/32, crcf."""
     metric = "Msamples/sec 32-branch polyphase decimator (M=32, 8 taps/branch); % HBM roofline"
     tol = 1e-6
@@ -270,17 +302,13 @@ class Cfg4Decim:
                                      algo=sd.ALGO_FMA)
         self.d_in = torch.empty(self.n, dtype=torch.complex64, device="cuda")
         self.d_out = torch.empty(self.n // 32 + 1, dtype=torch.complex64, device="cuda")
-        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, 2 * self.n,
-                                       torch.cuda.current_stream().cuda_stream)
+        self.time_sharded(args, rank, torch, sd, P_halo=lambda P: P.decim_halo(256, 32), m_per_in=32)
         self.samples_per_step = self.n
         self.bytes_per_step = 8 * self.n + 8 * (self.n // 32)
         self.dtype = "c32 (f32 taps x complex-f32 samples)"
         self.kernel = "decim_poly_kernel (column-parallel polyphase, fused multiply-add)"
         self.workload = f"cfg4: M=32 x 8-tap polyphase decimator, crcf, 2^{args.log2n} input samples per channel"
         self.algo_name = "fma"
-
-    def step(self, stream):
-        self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
 
     def parity(self, stream, rng, width=4096):
         """random windows of outputs recomputed in f64 from the definition
@@ -317,8 +345,11 @@ class Cfg4Decim:
         return sliding_window_view(xs, len(h))[::32][:width] @ np.asarray(h, np.float64) / 32.0
 
     def check_gathered(self, big, rng, width=4096):
-        """every rank's gathered decimated output (channel = rank), two random windows each"""
+        """every rank's gathered decimated output (channel = rank), two random windows each;
+        time-sharded: windows of the one stream inside and across the segments"""
         from solid_dsp_amd import parallel as P
+        if self.shard == "time":
+            return P.check_time_sharded(big, lambda g, w: Cfg4Decim.expected(self.h, 0, g, w), rng, width, 8)
         return P.check_gathered(big, lambda r, m, w: Cfg4Decim.expected(self.h, r, m, w), rng, width, 8,
                                 self.n // 32)
 
@@ -964,17 +995,25 @@ def dry_run(args, rank, world):
         expected = lambda r, m, w: Cfg4Decim.expected(h, r, m, w)
         lo, hi, width = 8, n // 32, 256
     t0 = time.perf_counter()
-    y = run(O.synth(SEED, rank, 0, n, complex_=True).astype(np.complex128)).astype(np.complex64)
+    if args.shard == "time":  # segment `rank` of one stream after its halo (the GPU path's StreamShard)
+        mpi = 1 if cfg == 2 else 32
+        first, hh = P.time_segment(n, rank, P.fir_halo(256) if cfg == 2 else P.decim_halo(256, 32))
+        y = run(O.synth(SEED, 0, first, hh + n, complex_=True).astype(np.complex128))[hh // mpi:].astype(np.complex64)
+    else:
+        y = run(O.synth(SEED, rank, 0, n, complex_=True).astype(np.complex128)).astype(np.complex64)
     if os.environ.get("SDSP_DRYRUN_FAULT") == "shift" and rank == world - 1:
         y = np.concatenate([np.zeros(1, np.complex64), y[:-1]])
     wall = P.max_over_ranks(time.perf_counter() - t0)
     ranks = P.gather_to_root(torch.tensor([rank], dtype=torch.int64), 0)
     big = P.gather_full_to_root(torch.from_numpy(y), 0, chunk_bytes=1 << 14)
     if rank == 0:
-        worst = P.check_gathered(big, expected, np.random.default_rng(2), width, lo, hi)
+        if args.shard == "time":
+            worst = P.check_time_sharded(big, lambda g, w: expected(0, g, w), np.random.default_rng(2), width, lo)
+        else:
+            worst = P.check_gathered(big, expected, np.random.default_rng(2), width, lo, hi)
         print(json.dumps({"metric": "dry-run: rank launch + max-over-ranks timing + full gather + gathered-output "
                           "check (gloo, CPU)", "value": world * n / wall / 1e6, "unit": "Msamples/sec",
-                          "n_gpus": world, "config": cfg, "ranks": [int(t.item()) for t in ranks],
+                          "n_gpus": world, "config": cfg, "shard": args.shard, "ranks": [int(t.item()) for t in ranks],
                           "gather_rows": int(big.shape[0]), "gather_check": worst,
                           "gather_ok": bool(worst <= 1e-6), "dry_run": True}), flush=True)
     if world > 1:
@@ -989,6 +1028,8 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     if args.gpus is not None and args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.shard == "time" and args.config not in (2, 4):
+        sys.exit("bench.py: --shard time applies to configs 2 (FIR) and 4 (decimator)")
     if args.dry_run:
         return dry_run(args, rank, world)
 
@@ -1077,9 +1118,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": w.dtype,
-            "data": "synthetic SplitMix64 stream (seed 20250226, channel = rank), device generated",
+            "data": ("synthetic SplitMix64 stream (seed 20250226, channel = rank), device generated"
+                     if getattr(w, "shard", "channel") != "time" else
+                     "synthetic SplitMix64 stream (seed 20250226, one channel; rank r generates its segment and halo), "
+                     "device generated"),
             "config": {"workload": w.workload, "samples_per_step_per_gpu": w.samples_per_step,
-                       "kernel": w.kernel, "parallelism": f"channels sharded, independent per GPU x {world}"},
+                       "kernel": w.kernel,
+                       "parallelism": getattr(w, "parallelism", None) or f"channels sharded, independent per GPU x {world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,

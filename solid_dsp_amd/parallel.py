@@ -1,7 +1,8 @@
 """Multi-GPU harness for the engine: one process per GPU,
 independent channels/streams sharded across ranks with no data-path
-collective, max-over-ranks timing, and an RCCL gather of results to rank 0
-after the timed region.
+collective -- or one long FIR / decimator stream time-sharded, each rank
+reading its segment plus a halo of preceding inputs -- max-over-ranks timing,
+and an RCCL gather of results to rank 0 after the timed region.
 
 Backend-agnostic on purpose: bench.py runs it over RCCL ("nccl") with device
 tensors; tests/test_parallel_gloo.py runs the same functions over gloo with
@@ -126,4 +127,57 @@ def check_gathered(big, expected, rng, width: int, lo: int, hi: int, windows: in
             if got.shape != ref.shape:
                 return float("inf")
             worst = max(worst, float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-300)))
+    return worst
+
+
+# ---------------------------------------------------------------------------
+# Time-sharding one long stream: rank r filters the global inputs
+# [r n, (r + 1) n) of a single stream.  A FIR output depends on the L - 1 inputs
+# before it only, so the rank first feeds `halo` preceding inputs to a fresh
+# handle (their outputs are dropped) and its outputs are then exactly the single
+# stream's; no exchange.  A decimator's halo is a multiple of M, so the fresh
+# handle's phase lines up with the global one (segments start at multiples of M).
+
+def fir_halo(taps: int) -> int:
+    """inputs a FIR segment reads before its own (the delay line, fir/mod.rs:209-212)"""
+    return taps - 1
+
+
+def decim_halo(taps: int, M: int) -> int:
+    """the delay line rounded up to whole decimation periods (decim.rs:221-228): the
+    fresh handle's phase 0 falls on a global multiple of M"""
+    return -(-(taps - 1) // M) * M
+
+
+def time_segment(n: int, rank: int, halo: int):
+    """(first global input the rank reads, halo inputs actually read): rank 0 starts
+    the stream from the zero state, so it reads no halo"""
+    h = min(halo, rank * n)
+    return rank * n - h, h
+
+
+def check_time_sharded(big, expected, rng, width: int, lo: int, windows: int = 2) -> float:
+    """Worst relative RMS error of the gathered outputs of one time-sharded stream
+    ([ranks, m] rows, row r = global outputs [r m, (r + 1) m)) against
+    expected(global_first_output, width): `windows` random windows inside every row
+    (global index >= lo), and one window across every boundary between two rows --
+    where a wrong halo or phase would show."""
+    import numpy as np
+    rows, m = big.shape[0], big.shape[1]
+    flat = big.reshape(-1)
+    starts = []
+    for r in range(rows):
+        a = max(lo, r * m)
+        for _ in range(windows):
+            starts.append(int(rng.integers(a, (r + 1) * m - width + 1)))
+        if r > 0:
+            starts.append(r * m - width // 2)
+    worst = 0.0
+    for g in starts:
+        ref = np.asarray(expected(g, width), dtype=np.complex128)
+        got = flat[g:g + width]
+        got = np.asarray(got.cpu().numpy() if hasattr(got, "cpu") else got, dtype=np.complex128)
+        if got.shape != ref.shape:
+            return float("inf")
+        worst = max(worst, float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-300)))
     return worst

@@ -712,3 +712,49 @@ def test_host_step_is_fast():
         f.execute(v)
     us = (time.perf_counter() - t0) / len(x) * 1e6
     assert us < 20.0, us  # through ctypes; the C call itself is measured by bench.py (dropin)
+
+
+@pytest.mark.parametrize("algo", ["exact", "fast"])
+@pytest.mark.parametrize("M", [1, 32])
+def test_time_sharded_stream_on_device(algo, M):
+    """SURVEY §8e time-sharding as bench.py --shard time runs it (StreamShard): segments
+    of one cfg2 / cfg4 stream, each on a fresh handle after its halo (parallel.time_segment)
+    with device-resident blocks, concatenate to the single-stream device output --
+    bit-identical on the EXACT kernels, within the §8d tolerance on the fast ones
+    (overlap-save / polyphase FMA, whose block boundaries move with the call)"""
+    import torch
+    from solid_dsp_amd import parallel as P
+    from solid_dsp_amd.filter import firdes
+    n, R = 1 << 16, 3
+    x = O.synth(20250226, 0, 0, R * n, complex_=True).astype(np.complex64)
+    if M == 1:
+        h, s = firdes.firdes_kaiser(256, 0.1, 80.0, 0.0).astype(np.float32), np.float32(0.2)
+        mk = lambda: FIRFilter(h, s, sample_dtype=np.complex64, algo=sd.ALGO_EXACT if algo == "exact" else sd.ALGO_FFT)
+        halo = P.fir_halo(256)
+    else:
+        h, s = firdes.firdes_kaiser(256, 1.0 / 64, 80.0, 0.0).astype(np.float32), np.float32(1.0 / 32)
+        mk = lambda: DecimatingFIRFilter(h, s, M, sample_dtype=np.complex64,
+                                         algo=sd.ALGO_EXACT if algo == "exact" else sd.ALGO_FMA)
+        halo = P.decim_halo(256, M)
+    st = torch.cuda.current_stream()
+
+    def run(f, xs):
+        d_in = to_dev(xs)
+        d_out = empty_dev(max(f.output_count(len(xs)), 1), np.complex64)
+        k = f.execute_block_device(d_in, len(xs), d_out, st)
+        return to_host(d_out)[:k]
+
+    full = run(mk(), x)
+    segs = []
+    for r in range(R):
+        first, hh = P.time_segment(n, r, halo)
+        f = mk()
+        if hh:
+            run(f, x[first:r * n])  # the halo: outputs dropped
+        segs.append(run(f, x[r * n:(r + 1) * n]))
+    got = np.concatenate(segs)
+    assert len(got) == len(full)
+    if algo == "exact":
+        assert bits_equal(got, full)
+    else:
+        assert rel_rms(got, full) <= 1e-6
