@@ -35,7 +35,8 @@
 // 16-column block; rows 544 dwords apart, i.e. opposite halves of the 64
 // banks).  Every access is a per-lane base plus a compile-time offset and is
 // conflict-free except P5's reads (lanes 0 and 31 of a 32-lane group share a
-// bank pair: 3 LDS cycles instead of 2).
+// bank pair: SQ_LDS_BANK_CONFLICT counts 2 extra cycles per ds_read_b64,
+// tools/lds_probe.hip).
 //
 // Numerics: bit-identical across calls and launch shapes; against the f64
 // restatement rel-RMS ~1.8e-7 on the cfg2 taps (§8d tolerance 1e-6).
