@@ -97,10 +97,16 @@ __device__ __forceinline__ unsigned int* cu_slot() {
 // per-CU ticket taken with vector atomics before the loads, returned once P1
 // has consumed them); 32: high wave priority while issuing loads and stores; 128:
 // plain (not nontemporal) stores.
-template <int VAR>
+// STG (lab, the staggered pair kernel): 0 one segment per workgroup; 1 / 2 the first /
+// second half of a 512-lane workgroup running two segments, the second starting its
+// loads at the barrier that ends the first half's P1 (three workgroup barriers per
+// half: 1 = P1 | P4 | end, 2 = start | P1 | P4).  `active` false: no loads or stores,
+// the barriers only (the last pair of a range with an odd count).
+template <int VAR, int STG = 0>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
-                                               int h2, f2* img, int t) {
+                                               int h2, f2* img, int t, bool active = true) {
+    if constexpr (STG == 2) __syncthreads();  // the first half's P1 is done: its loads have landed
     const int hi4 = t >> 4, lo4 = t & 15;
 #ifdef SDSP_OLS_LAB
     constexpr unsigned kLim = (VAR >> 3) & 3;
@@ -130,6 +136,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         if constexpr (VAR & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
+        else if constexpr (STG != 0) v[r] = active ? __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0)) : f2{0.0f, 0.0f};
         else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
     }
 #ifdef SDSP_OLS_LAB
@@ -243,8 +250,9 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     constexpr int kStAux = (VAR & 128) ? 0 : 2;
 #pragma unroll
     for (int r = 0; r < 16; ++r)
-        if (r >= h2)
+        if (r >= h2 && (STG == 0 || active))
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, kStAux);
+    if constexpr (STG == 1) __syncthreads();  // the second half's P4 -> P5 barrier
 }
 
 #ifdef SDSP_OLS_LAB  // lab only: measured slower than the one-shot kernel
@@ -525,6 +533,27 @@ fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const
 }
 
 #ifdef SDSP_OLS_LAB
+// Staggered pair (lab): a 512-lane workgroup runs segments s and
+// s + 1 of its XCD eighth in two 256-lane halves, the second half's loads issued only
+// after the first half's P1 -- at most one segment's loads in flight per workgroup, two
+// workgroups (16 waves) per CU, no atomics.
+template <int VAR>
+__global__ void __launch_bounds__(512, 2)
+fir_ols_pair_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
+                    f2* __restrict__ y, long long n, long long lo, long long hi, long long q, int h2) {
+    __shared__ __attribute__((aligned(16))) f2 img[2][16 * kRow];
+    const int xc = blockIdx.x & 7;
+    const long long s0 = lo + (long long)xc * q + 2 * (long long)(blockIdx.x >> 3);
+    const long long xe0 = lo + (long long)(xc + 1) * q, xe = xe0 < hi ? xe0 : hi;
+    if (s0 >= xe) return;  // uniform over the workgroup
+    const int V = 4096 - 256 * h2;
+    const int half = threadIdx.x >> 8, t = threadIdx.x & 255;  // wave-uniform
+    const long long seg = s0 + half;
+    const long long base = (long long)blockIdx.y * n + (seg < xe ? seg : s0) * V - 256 * h2;
+    if (half == 0) ols_os_segment<VAR, 1>(x, Hs, tb, y, base, h2, img[0], t, true);
+    else ols_os_segment<VAR, 2>(x, Hs, tb, y, base, h2, img[1], t, seg < xe);
+}
+
 static int g_lab_variant = 0, g_lab_lds = 0, g_lab_tok = 0;
 extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int lds, int tok) {
     g_lab_variant = v;
@@ -554,7 +583,14 @@ hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n,
     const long long q = (hi - lo + 7) / 8;
     const dim3 grid((unsigned)(8 * q), (unsigned)channels);
 #ifdef SDSP_OLS_LAB
-    if (g_lab_variant >= 256) {  // slot kernel: 256 + 16 ablation + SLOTS (3 or 4); lds field = workgroups per eighth
+    if (g_lab_variant == 512) {  // staggered pair kernel
+        const long long q2 = (q + 1) / 2;
+        hipLaunchKernelGGL(fir_ols_pair_kernel<0>, dim3((unsigned)(8 * q2), (unsigned)channels), dim3(512), 0, s,
+                           (const f2*)x, (const float4*)p.d_pkt, (const float4*)p.d_ostab, (f2*)y, (long long)n, lo,
+                           hi, q, p.halo_rows);
+        return hipGetLastError();
+    }
+    if (g_lab_variant >= 256 && g_lab_variant < 512) {  // slot kernel: 256 + 16 ablation + SLOTS (3 or 4); lds field = workgroups per eighth
         const int slots = g_lab_variant & 15;
         const int J = g_lab_lds > 0 ? g_lab_lds : 32;
         const dim3 g2(8 * J, (unsigned)channels);
