@@ -259,7 +259,7 @@ class Cfg3IIR:
         self.samples_per_step = self.n
         self.bytes_per_step = 8 * self.n
         self.dtype = "f32 (f32 coefficients, real f32 samples)"
-        self.kernel = "sos_wscan_kernel<4> (wave-level scan, 256-byte chunks, state-response correction)"
+        self.kernel = "sos_wscan_kernel<4> (wave-level scan, 128-byte chunks, state-response correction)"
         self.workload = f"cfg3: 4-biquad SOS cascade butter(8, 0.2), real f32, 2^{args.log2n} samples per channel"
         self.algo_name = "scan"
 

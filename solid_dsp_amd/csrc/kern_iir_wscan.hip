@@ -162,7 +162,10 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // Mi > 1 the staged domain sample k is x[k / Mi] at k % Mi == 0, else zero; with
 // Md > 1 only domain samples k = j0 + o Md are stored, as y[o] (gathered from the
 // slab so that 64 consecutive outputs leave per store instruction).
-template <int S, int ND, typename C, typename I, int CB, bool RERUN>
+// FORM: 0 correction by the state response, next tile prefetched into registers; 1 a
+// rerun from the true state instead of the correction; 2 the correction without the
+// register prefetch (fewer registers: more waves per SIMD hide the tile loads instead)
+template <int S, int ND, typename C, typename I, int CB, int FORM>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
@@ -171,6 +174,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                  long long nwaves) {
     constexpr int D = ND ? ND : 2 * S;
     constexpr int B = ws_chunk<I, CB>::B;
+    constexpr bool RERUN = FORM == 1, PF = FORM != 2;
     constexpr int E = 16 / (int)sizeof(I);  // samples per 16-byte vector
     constexpr int kRowBytes = WsGeom<CB>::kRowBytes, kVecPerRow = WsGeom<CB>::kVecPerRow;
     constexpr int kSlabBytes = WsGeom<CB>::kSlabBytes;
@@ -221,7 +225,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     // the compute (a per-vector branch would serialise the HBM round trips)
     auto interior_at = [&](long long k0) { return vec_ok && Mi == 1 && k0 >= 0 && k0 + 64LL * B <= nd; };
     v4u pre[kVecPerRow];
-    {
+    if constexpr (PF) {
         const long long k0 = (c_lo - wc) * B;
         if (interior_at(k0)) {
 #pragma unroll
@@ -239,6 +243,13 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         // 1. stage the tile: vector v of the tile -> row v / kVecPerRow, slot v % kVecPerRow
         const bool interior = interior_at(k0);
         if (interior) {
+            if constexpr (!PF) {
+#pragma unroll
+                for (int j = 0; j < kVecPerRow; ++j)
+                    pre[j] = (lab & 8)    ? v4u{(unsigned)lane, (unsigned)t, 0u, (unsigned)j}
+                             : (lab & 32) ? reinterpret_cast<const v4u*>(x + k0)[lane + 64 * j]
+                                          : __builtin_nontemporal_load(reinterpret_cast<const v4u*>(x + k0) + lane + 64 * j);
+            }
 #pragma unroll
             for (int j = 0; j < kVecPerRow; ++j) {
                 const int v = lane + 64 * j;
@@ -254,7 +265,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 *reinterpret_cast<v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16) = to_v4<I>(tmp);
             }
         }
-        {  // prefetch the next tile (whatever path this one took)
+        if constexpr (PF) {  // prefetch the next tile (whatever path this one took)
             const long long kn = k0 + 64LL * B;
             if (t + 1 < tpw && interior_at(kn)) {
 #pragma unroll
@@ -795,7 +806,7 @@ template <int CB> int wscan_tpw(long long nch) {
     return tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
 }
 
-template <typename C, typename I, int S, int CB, bool RERUN, int ND = 0>
+template <typename C, typename I, int S, int CB, int FORM, int ND = 0>
 hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     constexpr int B = ws_chunk<I, CB>::B;
     constexpr int D = ND ? ND : 2 * S;
@@ -818,31 +829,31 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     const long long j0 = a.Md > 1 ? (long long)((a.Md - 1 - a.phase) % a.Md) : 0;  // first emitting domain index
     const long long ny = a.Md > 1 ? (long long)a.nout : nd;
     if (exact) {
-        hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
+        hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
                            (I*)a.y, (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out,
                            nd, 0, tpw, vec_ok, a.Mi, a.Md, j0, ny, (const I*)nullptr, (I*)a.G, waves);
         hipLaunchKernelGGL((wscan_carry_kernel<D, C, I>), dim3((unsigned)a.channels), dim3(256), 0, st,
                            (const I*)a.G, (I*)a.Cin, (const C*)a.Phi + (size_t)(tpw - 1) * D * D, (const I*)a.st_in,
                            waves);
     }
-    hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, RERUN>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
+    hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
                        tpw, vec_ok, a.Mi, a.Md, j0, ny, exact ? (const I*)a.Cin : (const I*)nullptr, (I*)nullptr,
                        waves);
     return hipGetLastError();
 }
 
-template <typename C, typename I, int CB, bool RERUN = false>
+template <typename C, typename I, int CB, int FORM = 0>
 hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
     switch (a.sections) {
-        case 1: return launch_wscan_t<C, I, 1, CB, RERUN>(a, st);
-        case 2: return launch_wscan_t<C, I, 2, CB, RERUN>(a, st);
-        case 3: return launch_wscan_t<C, I, 3, CB, RERUN>(a, st);
-        case 4: return launch_wscan_t<C, I, 4, CB, RERUN>(a, st);
-        case 5: return launch_wscan_t<C, I, 5, CB, RERUN>(a, st);
-        case 6: return launch_wscan_t<C, I, 6, CB, RERUN>(a, st);
-        case 7: return launch_wscan_t<C, I, 7, CB, RERUN>(a, st);
-        case 8: return launch_wscan_t<C, I, 8, CB, RERUN>(a, st);
+        case 1: return launch_wscan_t<C, I, 1, CB, FORM>(a, st);
+        case 2: return launch_wscan_t<C, I, 2, CB, FORM>(a, st);
+        case 3: return launch_wscan_t<C, I, 3, CB, FORM>(a, st);
+        case 4: return launch_wscan_t<C, I, 4, CB, FORM>(a, st);
+        case 5: return launch_wscan_t<C, I, 5, CB, FORM>(a, st);
+        case 6: return launch_wscan_t<C, I, 6, CB, FORM>(a, st);
+        case 7: return launch_wscan_t<C, I, 7, CB, FORM>(a, st);
+        case 8: return launch_wscan_t<C, I, 8, CB, FORM>(a, st);
     }
     return hipErrorInvalidValue;
 }
@@ -851,14 +862,14 @@ hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
 template <typename C, typename I>
 hipError_t launch_wscan_normal(const IirArgs& a, hipStream_t st) {
     switch (a.cap - 1) {
-        case 1: return launch_wscan_t<C, I, 0, 256, false, 1>(a, st);
-        case 2: return launch_wscan_t<C, I, 0, 256, false, 2>(a, st);
-        case 3: return launch_wscan_t<C, I, 0, 256, false, 3>(a, st);
-        case 4: return launch_wscan_t<C, I, 0, 256, false, 4>(a, st);
-        case 5: return launch_wscan_t<C, I, 0, 256, false, 5>(a, st);
-        case 6: return launch_wscan_t<C, I, 0, 256, false, 6>(a, st);
-        case 7: return launch_wscan_t<C, I, 0, 256, false, 7>(a, st);
-        case 8: return launch_wscan_t<C, I, 0, 256, false, 8>(a, st);
+        case 1: return launch_wscan_t<C, I, 0, 256, 0, 1>(a, st);
+        case 2: return launch_wscan_t<C, I, 0, 256, 0, 2>(a, st);
+        case 3: return launch_wscan_t<C, I, 0, 256, 0, 3>(a, st);
+        case 4: return launch_wscan_t<C, I, 0, 256, 0, 4>(a, st);
+        case 5: return launch_wscan_t<C, I, 0, 256, 0, 5>(a, st);
+        case 6: return launch_wscan_t<C, I, 0, 256, 0, 6>(a, st);
+        case 7: return launch_wscan_t<C, I, 0, 256, 0, 7>(a, st);
+        case 8: return launch_wscan_t<C, I, 0, 256, 0, 8>(a, st);
     }
     return hipErrorInvalidValue;
 }
@@ -867,12 +878,15 @@ template <typename C, typename I>
 hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
     if (a.sections == 0) return launch_wscan_normal<C, I>(a, st);
     if (a.Mi != 1 || a.Md != 1 || a.wc == 0)  // rate changes / exact carries: the single-chunk kernels only
-        return a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st) : launch_wscan_s<C, I, 256>(a, st);
+        return a.ws_variant == 5   ? launch_wscan_s<C, I, 128, 2>(a, st)
+               : a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st)
+                                   : launch_wscan_s<C, I, 256>(a, st);
     if constexpr (std::is_same<I, float>::value) {
         if (a.ws_variant == 2) return launch_wscan2_s<128>(a, st);
         if (a.ws_variant == 3) return launch_wscan2_s<64>(a, st);
     }
-    if (a.ws_variant == 4) return launch_wscan_s<C, I, 256, true>(a, st);  // rerun instead of correction
+    if (a.ws_variant == 4) return launch_wscan_s<C, I, 256, 1>(a, st);  // rerun instead of correction
+    if (a.ws_variant == 5) return launch_wscan_s<C, I, 128, 2>(a, st);  // 128-byte chunks, no register prefetch
     return a.ws_variant == 1 ? launch_wscan_s<C, I, 128>(a, st) : launch_wscan_s<C, I, 256>(a, st);
 }
 
@@ -886,10 +900,11 @@ extern "C" __attribute__((visibility("default"))) int sdsp_lab_set_iir_ablation(
 #endif
 
 size_t iir_wscan_waves(int dtype, const IirArgs& a, int* tpw_out) {
-    const int B = iir_wscan_chunk(dtype, a.ws_variant == 1 ? 1 : 0);
+    const bool c128 = a.ws_variant == 1 || a.ws_variant == 5;
+    const int B = iir_wscan_chunk(dtype, c128 ? 1 : 0);
     if (B == 0) return 0;
     const long long nch = ((long long)a.n * a.Mi + B - 1) / B;
-    const int tpw = a.ws_variant == 1 ? wscan_tpw<128>(nch) : wscan_tpw<256>(nch);
+    const int tpw = c128 ? wscan_tpw<128>(nch) : wscan_tpw<256>(nch);
     if (tpw_out) *tpw_out = tpw;
     const long long segc = (long long)tpw * 64 - a.wc;
     return (size_t)((nch + segc - 1) / segc);
@@ -897,7 +912,8 @@ size_t iir_wscan_waves(int dtype, const IirArgs& a, int* tpw_out) {
 
 int iir_wscan_chunk(int dtype, int variant) {
     // variants: 0 = 256-byte chunks, 1 = 128-byte, 2/3 = paired 128/64-byte chunks (real f32 only),
-    // 4 = 256-byte chunks with a rerun instead of the state-response correction
+    // 4 = 256-byte chunks with a rerun instead of the state-response correction, 5 = 128-byte
+    // chunks without the register prefetch
     if ((variant == 2 || variant == 3) && dtype != 0) return 0;
     const int cb = (variant == 0 || variant == 4) ? 256 : (variant == 3 ? 64 : 128);
     switch (dtype) {

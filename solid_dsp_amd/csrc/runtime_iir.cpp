@@ -40,7 +40,7 @@ struct Group {
         DevBuf d_P, d_Cr;      // [6][2c][2c], [B][2c] output response to the state
         DevBuf d_Phi;          // exact carries: [8][2c][2c] A^(64 B t), t = 1..8
         long long phi_wmax[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // per tpw: waves the carry chain admits
-    } ws[5];
+    } ws[6];
 };
 
 struct DeviceGuardI {
@@ -104,7 +104,7 @@ struct sdsp_iir {
     DevBuf d_coefs, d_coefs_nrm, d_state[2], d_tmp[2], d_carry[2];
     int cur = 0;
     int algo = SDSP_ALGO_EXACT;  // reference-order recurrence unless the caller opts in (sdsp.h)
-    int wscan = 1;  // 0: block scan; 1-4: wave-scan variant 0-3 (kern_iir_wscan.hip; sdsp_iir_set_tuning)
+    int wscan = 1;  // 0: block scan; 1-6: wave-scan variant 0-5 (kern_iir_wscan.hip; sdsp_iir_set_tuning)
     hipStream_t stream = nullptr;
     mutable StreamFence fence;  // last caller stream an execute call was queued on
     DevBuf stage_in, stage_out;
@@ -383,7 +383,7 @@ int plan_groups(sdsp_iir* h) {
         if (st) return st;
         // wave scan (kern_iir_wscan.hip), one table set per chunk size: 6 powers, warm-up <= 32
         // chunks; without a decaying state response the single-chunk variants carry exactly
-        for (int v = 0; v < 5; ++v) {
+        for (int v = 0; v < 6; ++v) {
             const int Bw = iir_wscan_chunk(h->dtype, v);
             if (Bw == 0) continue;
             if (g.wc == 0 && v != 0 && v != 1) continue;
@@ -434,6 +434,9 @@ int iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void
     h->dtype = dtype;
     h->device = device;
     h->type = type;
+    // real f32: 128-byte chunks (B = 32; cfg3 1.75 -> 1.72 ms, its compute-only ablation 1.63 ->
+    // 1.40 ms); wider samples keep 256-byte chunks so a chunk holds >= 16 samples per scan
+    h->wscan = dtype == SDSP_RR32 ? 2 : 1;
     h->mode = mode;
     h->M = mode ? M : 1;
     h->ff.assign((const unsigned char*)ff, (const unsigned char*)ff + nff * cb);
@@ -599,7 +602,7 @@ int sdsp_iir_set_algo(sdsp_iir* h, int algo) {
 int sdsp_iir_set_tuning(sdsp_iir* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (key != SDSP_TUNE_IIR_WAVE_SCAN) return SDSP_E_INVALID_ARGUMENT;
-    if (value < 0 || value > 5) return SDSP_E_INVALID_ARGUMENT;
+    if (value < 0 || value > 6) return SDSP_E_INVALID_ARGUMENT;
     h->wscan = value;
     return SDSP_OK;
 }

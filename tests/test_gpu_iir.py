@@ -194,10 +194,11 @@ def test_scan_cfg3_cascade_tolerance(dt, cdt, sdt):
 
 
 @pytest.mark.parametrize("dt,cdt,sdt", DT)
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_scan_kernel_variants(dt, cdt, sdt, variant):
     # block scan (0) and the wave-scan variants (1: 256-byte chunks, 2: 128-byte, 3/4: paired
-    # 128/64-byte chunks, real f32 only; elsewhere the handle falls back to the block scan):
+    # 128/64-byte chunks, real f32 only; elsewhere the handle falls back to the block scan;
+    # 5: rerun instead of correction; 6: 128-byte chunks without the register prefetch):
     # many segments, ragged streaming calls, against the f64 restatement
     ff, fb = butter()
     f = IIRFilter(ff.astype(cdt), fb.astype(cdt), SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
@@ -214,7 +215,7 @@ def test_scan_kernel_variants(dt, cdt, sdt, variant):
     assert np.abs(y - ref).max() <= tol * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6])
 def test_scan_multi_tile_segments(variant):
     # 2^26 real f32 samples: several tiles per wave (cross-tile carry, prefetch), checked
     # against the block scan on the whole stream and the f64 restatement on its head and tail
