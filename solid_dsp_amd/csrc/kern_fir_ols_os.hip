@@ -554,6 +554,393 @@ fir_ols_pair_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, con
     else ols_os_segment<VAR, 2>(x, Hs, tb, y, base, h2, img[1], t, seg < xe);
 }
 
+// Trio kernel (lab): one 768-lane workgroup per CU, three 256-lane slots, each
+// running its segments through three stages; stages end at workgroup barriers
+// (plain s_barrier, LDS waits only: loads and stores stay in flight):
+//   S0  P5 and the stores of the current segment, then P1 of the next one
+//       (lane-owned columns: P5's reads and P1's writes touch only the lane's own)
+//   S1  P2 and the forward half of P3 (DFT16 n0 -> k2, * H)
+//   S2  the inverse half of P3 and P4; the loads of the segment after are issued
+// Slot s runs stage (t - s + 2) mod 3 at tick t (none before tick s): each tick
+// one slot of the CU has segment loads in flight and one stores, while all 12
+// waves compute.  Segments come from a per-XCD-eighth counter (one returning
+// atomic per segment, fetched a stage before its loads): the segments a CU's
+// XCD has in flight stay neighbours, as in the one-shot dispatch order.
+struct OlsTrioShared {
+    f2 img[3][16 * kRow];
+    float4 hq[8][256];  // spectrum slices of P3, [k-pair][lane] (shared by the slots)
+    int nidx[3];
+};
+__device__ unsigned long long g_ols_trio_q[2][8 * 16];
+
+__device__ __forceinline__ void trio_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ long long pick3(const long long (&a)[3], int s) { return s == 0 ? a[0] : s == 1 ? a[1] : a[2]; }
+
+// ABL: 0 full, 1 HBM traffic only (rows stored as loaded), 2 compute only (no loads, stores dropped)
+template <int ABL>
+__global__ void __launch_bounds__(768, 1)
+fir_ols_trio_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
+                    f2* __restrict__ y, long long lo, long long hi, long long q, int h2, int par) {
+    __shared__ __attribute__((aligned(16))) OlsTrioShared sh;
+    const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+    const int t = threadIdx.x & 255, hi4 = t >> 4, lo4 = t & 15;
+    const int xc = blockIdx.x & 7, J = gridDim.x >> 3, jb = blockIdx.x >> 3;
+    const long long s0 = lo + (long long)xc * q, se0 = s0 + q, se = se0 < hi ? se0 : hi;
+    const int cnt = se > s0 ? (int)(se - s0) : 0;
+    const int V = 4096 - 256 * h2;
+    unsigned long long* ctr = &g_ols_trio_q[par][16 * xc];
+    if (blockIdx.x == 0 && threadIdx.x < 8)  // the next launch's counters (the previous launch used them)
+        __hip_atomic_store(&g_ols_trio_q[par ^ 1][16 * threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
+    const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0, 2048 * 16, kBufWord3);
+    const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 0, 0));
+    const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 4096, 0));
+    const float4 b2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 8192, 0));
+    f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
+    f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
+    f2* img = sh.img[slot];
+    f2* col = img + t + (t >> 4);
+    f2* r2 = img + hi4 * kRow + lo4;
+    f2* r3 = img + hi4 * kRow + 17 * lo4;
+
+    // every wave tracks all three slots (uniform): current and next segment (cnt = none) and the
+    // stage each slot runs in the current tick (-1 before its first tick; then 2, 0, 1, 2, 0, ...)
+    int cur[3], nxt[3], ph[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        cur[s] = cnt;
+        nxt[s] = 3 * jb + s < cnt ? 3 * jb + s : cnt;
+        ph[s] = s == 0 ? 2 : -1;
+    }
+    const int myc0 = 0;
+    (void)myc0;
+    auto mine = [&](const int (&a)[3]) { return slot == 0 ? a[0] : slot == 1 ? a[1] : a[2]; };
+    // a segment's buffer descriptors; none (num_records 0: loads return 0, stores are dropped) past the eighth
+    auto seg_rsrc = [&](const f2* base, int k) {
+        const bool ok = (unsigned)k < (unsigned)cnt;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (s0 + (ok ? k : 0)) * V - 256 * h2), (short)0,
+                                                 ok ? 32768 : 0, kBufWord3);
+    };
+    // loop invariants: the spectrum slices in LDS, W256^(lo4 k) in registers
+    for (int i = threadIdx.x; i < 8 * 256; i += 768)
+        sh.hq[i >> 8][i & 255] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * (i & 255), 4096 * (i >> 8), 0));
+    f2 w2[16];
+    {
+        const float4 e0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12288, 0));
+        const float4 e1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12544, 0));
+        const float4 e2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12800, 0));
+        const f2 Eb[3] = {f2{e0.x, e0.y}, f2{e0.z, e0.w}, f2{e1.x, e1.y}};
+        const f2 Fa[3] = {f2{e1.z, e1.w}, f2{e2.x, e2.y}, f2{e2.z, e2.w}};
+        w2[0] = f2{1.0f, 0.0f};
+#pragma unroll
+        for (int k = 1; k < 16; ++k) w2[k] = tw_pair(Eb, Fa, k);
+    }
+    __syncthreads();
+    f2 v[16], vn[16], u[16];
+    unsigned long long got = 0;
+
+    // S0: P5 and the stores of the current segment, then P1 of the next one (its loads were issued in S2)
+    auto stage0 = [&]() {
+        const auto ry = seg_rsrc(y, mine(cur));
+        if constexpr (ABL == 1) {
+            const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 0, kBufWord3);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[r]), r >= h2 ? ry : rz, 8 * t, 2048 * r, 2);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = vn[r];
+            return;
+        }
+        // P5: * conj W4096^(t k0), IDFT16 k0 -> n2
+#pragma unroll
+        for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Cb[i]), "+v"(Da[i]));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = k == 0 ? col[0] : pmulc(col[k * kRow], tw_pair(Cb, Da, k));
+        pdft16<true>(v);
+        if constexpr (ABL == 2) {
+            f2 acc = v[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) acc += v[r];
+            if (acc.x == 1.2345e30f) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc), ry, 8 * t, 0, 0);
+        } else {
+            // every row issues one store (halo rows to an empty descriptor: dropped), so that the
+            // count of memory operations younger than the next segment's loads is exact
+            const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 0, kBufWord3);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), r >= h2 ? ry : rz, 8 * t, 2048 * r, 2);
+        }
+        // P1 of the next segment: DFT16 n2 -> k0, * W4096^(t k0) -> (k0, t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = vn[r];
+        pdft16<false>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) col[k * kRow] = k == 0 ? v[0] : pmul(v[kout(k)], tw_pair(Cb, Da, k));
+    };
+    // S1: P2 and the forward half of P3; the index of the segment after the next one
+    auto stage1 = [&]() {
+        if (t == 0 && mine(nxt) < cnt) got = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (ABL == 1) return;
+        // P2: lane (k0 = hi4, n0 = lo4): DFT16 n1 -> k1, * W256^(n0 k1)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
+        pdft16<false>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r2[17 * k] = k == 0 ? v[0] : pmul(v[kout(k)], w2[k]);
+        phase_sync<true>();
+        // P3, forward half: DFT16 n0 -> k2, * H
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = r3[j];
+        pdft16<false>(v);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const float4 h = sh.hq[p][t];
+            u[2 * p] = pmul(v[kout(2 * p)], f2{h.x, h.y});
+            u[2 * p + 1] = pmul(v[kout(2 * p + 1)], f2{h.z, h.w});
+        }
+    };
+    // S2: publish the fetched index, issue the loads of the next segment, then the inverse half of
+    // P3 and P4 of the current one
+    auto stage2 = [&]() {
+        const int mn = mine(nxt);
+        if (t == 0) sh.nidx[slot] = mn < cnt && got < (unsigned long long)cnt ? (int)min((unsigned long long)cnt, 3ull * J + got) : cnt;
+        const auto rx = seg_rsrc(x, mn);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if constexpr (ABL == 2) vn[r] = f2{1e-3f * t + r, 1e-9f * (float)mn};
+            else vn[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+        }
+        if constexpr (ABL == 1) return;
+        pdft16<true>(u);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) r3[j] = j == 0 ? u[kout(0)] : pmulc(u[kout(j)], w2[j]);
+        phase_sync<true>();
+        // P4: IDFT16 k1 -> n1
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
+        pdft16<true>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r2[17 * k] = v[kout(k)];
+    };
+
+    // a tick ends for every wave at one barrier; every slot that ran S0 in it moves on (the next
+    // segment becomes current, the published index next)
+    const int tick_cap = 3 * cnt + 16;  // a stale counter can only end the loop early, never hang it
+    int tick = 0;
+    auto end_tick = [&]() -> bool {
+        trio_barrier();
+        bool live = false;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            if (ph[s] == 0) {
+                cur[s] = nxt[s];
+                nxt[s] = nxt[s] < cnt ? __builtin_amdgcn_readfirstlane(sh.nidx[s]) : cnt;
+            }
+            ph[s] = ph[s] < 0 ? (tick + 1 == s ? 2 : -1) : (ph[s] == 2 ? 0 : ph[s] + 1);
+            live = live || ph[s] < 0 || cur[s] < cnt || nxt[s] < cnt;
+        }
+        ++tick;
+        return live && tick < tick_cap;
+    };
+    bool go = true;
+    for (int i = 0; i < slot && go; ++i) go = end_tick();
+    while (go) {
+        stage2();
+        if (!(go = end_tick())) break;
+        stage0();
+        if (!(go = end_tick())) break;
+        stage1();
+        go = end_tick();
+    }
+}
+
+// Quad kernel (lab): the trio's schedule with four 256-lane slots (16 waves per CU, as
+// many as the one-shot kernel) and four stages per segment:
+//   S0  P1 (its loads were issued two stages earlier); the queue index of the segment
+//       after the next
+//   S1  P2 and the forward half of P3 (spectrum slice and W256 bases from L2); the index
+//       is published in LDS
+//   S2  loads of the next segment, the inverse half of P3, P4
+//   S3  P5 and the stores
+// Slot s runs stage (t - s + 2) mod 4 at tick t.  Memory operations per slot in issue
+// order: S2 loads, S3 stores, S0 atomic, S1 table loads -- the only waits are P1's on
+// its loads (the 16 stores stay in flight) and S1's on its table loads (which also
+// drains the stores of two stages before).
+struct OlsQuadShared {
+    f2 img[4][16 * kRow];
+    int nidx[4];
+};
+__device__ unsigned int g_ols_quad_q[2][8 * 32];
+
+template <int ABL>
+__global__ void __launch_bounds__(1024, 1)
+fir_ols_quad_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
+                    f2* __restrict__ y, long long lo, long long hi, long long q, int h2, int par) {
+    __shared__ __attribute__((aligned(16))) OlsQuadShared sh;
+    constexpr int NS = 4;
+    const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+    const int t = threadIdx.x & 255, hi4 = t >> 4, lo4 = t & 15;
+    const int xc = blockIdx.x & 7, J = gridDim.x >> 3, jb = blockIdx.x >> 3;
+    const long long s0 = lo + (long long)xc * q, se0 = s0 + q, se = se0 < hi ? se0 : hi;
+    const int cnt = se > s0 ? (int)(se - s0) : 0;
+    const int V = 4096 - 256 * h2;
+    unsigned int* ctr = &g_ols_quad_q[par][32 * xc];
+    if (blockIdx.x == 0 && threadIdx.x < 8)  // the next launch's counters (the previous launch used them)
+        __hip_atomic_store(&g_ols_quad_q[par ^ 1][32 * threadIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+    const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
+    const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0, 2048 * 16, kBufWord3);
+    const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 0, kBufWord3);
+    const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 0, 0));
+    const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 4096, 0));
+    const float4 b2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 8192, 0));
+    f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
+    f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
+    f2* img = sh.img[slot];
+    f2* col = img + t + (t >> 4);
+    f2* r2 = img + hi4 * kRow + lo4;
+    f2* r3 = img + hi4 * kRow + 17 * lo4;
+
+    // every wave tracks all slots (uniform): current and next segment (cnt = none) and the stage
+    // each slot runs in the current tick (-1 before its first tick; then 2, 3, 0, 1, 2, ...)
+    int cur[NS], nxt[NS], ph[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        cur[s] = cnt;
+        nxt[s] = NS * jb + s < cnt ? NS * jb + s : cnt;
+        ph[s] = s == 0 ? 2 : -1;
+    }
+    auto mine = [&](const int (&a)[NS]) { return slot == 0 ? a[0] : slot == 1 ? a[1] : slot == 2 ? a[2] : a[3]; };
+    auto seg_rsrc = [&](const f2* base, int k) {
+        const bool ok = (unsigned)k < (unsigned)cnt;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (s0 + (ok ? k : 0)) * V - 256 * h2), (short)0,
+                                                 ok ? 32768 : 0, kBufWord3);
+    };
+    f2 v[16], vn[16], u[16], Eb[3], Fa[3];
+    float4 hq[8], e0, e1, e2;
+    unsigned int got = 0;
+
+    auto stage0 = [&]() {  // P1: DFT16 n2 -> k0, * W4096^(t k0) -> (k0, t); the queue fetch; S1's tables
+#pragma unroll
+        for (int p = 0; p < 8; ++p)
+            hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+        e0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12288, 0));
+        e1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12544, 0));
+        e2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12800, 0));
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = vn[r];
+        if constexpr (ABL == 1) return;
+        pdft16<false>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) col[k * kRow] = k == 0 ? v[0] : pmul(v[kout(k)], tw_pair(Cb, Da, k));
+    };
+    auto stage1 = [&]() {  // P2, P3 forward half; publish the fetched index
+        Eb[0] = f2{e0.x, e0.y}; Eb[1] = f2{e0.z, e0.w}; Eb[2] = f2{e1.x, e1.y};
+        Fa[0] = f2{e1.z, e1.w}; Fa[1] = f2{e2.x, e2.y}; Fa[2] = f2{e2.z, e2.w};
+        if constexpr (ABL == 1) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) u[j] = f2{0.0f, 0.0f};
+            return;
+        }
+        f2 w2[16];  // W256^(lo4 k); recomputed in S2 (the bases, not the 15 products, live across)
+        // P2: lane (k0 = hi4, n0 = lo4): DFT16 n1 -> k1, * W256^(n0 k1)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
+#pragma unroll
+        for (int k = 1; k < 16; ++k) w2[k] = tw_pair(Eb, Fa, k);
+        pdft16<false>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r2[17 * k] = k == 0 ? v[0] : pmul(v[kout(k)], w2[k]);
+        phase_sync<true>();
+        // P3, forward half: DFT16 n0 -> k2, * H
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = r3[j];
+        pdft16<false>(v);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            u[2 * p] = pmul(v[kout(2 * p)], f2{hq[p].x, hq[p].y});
+            u[2 * p + 1] = pmul(v[kout(2 * p + 1)], f2{hq[p].z, hq[p].w});
+        }
+    };
+    auto stage2 = [&]() {  // loads of the next segment; P3 inverse half, P4
+        const int mn = mine(nxt);
+        // the queue index of the segment after: issued before the loads, so that S3 can wait for it
+        // while the loads stay in flight
+        if (t == 0 && mn < cnt) got = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const auto rx = seg_rsrc(x, mn);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if constexpr (ABL == 2) vn[r] = f2{1e-3f * t + r, 1e-9f * (float)mn};
+            else vn[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+        }
+        if constexpr (ABL == 1) return;
+        pdft16<true>(u);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) r3[j] = j == 0 ? u[kout(0)] : pmulc(u[kout(j)], tw_pair(Eb, Fa, j));
+        phase_sync<true>();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
+        pdft16<true>(v);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) r2[17 * k] = v[kout(k)];
+    };
+    auto stage3 = [&]() {  // publish the fetched index; P5 and the stores (every row issues one: halo rows to an empty descriptor)
+        // dynamic indices follow the static round; anything past the eighth reads as none
+        if (t == 0) sh.nidx[slot] = mine(nxt) < cnt && got < (unsigned)cnt ? (int)min((unsigned)cnt, (unsigned)(NS * J) + got) : cnt;
+        const auto ry = seg_rsrc(y, mine(cur));
+        if constexpr (ABL != 1) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Cb[i]), "+v"(Da[i]));
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = k == 0 ? col[0] : pmulc(col[k * kRow], tw_pair(Cb, Da, k));
+            pdft16<true>(v);
+        }
+        if constexpr (ABL == 2) {
+            f2 acc = v[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) acc += v[r];
+            if (acc.x == 1.2345e30f) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc), ry, 8 * t, 0, 0);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[ABL == 1 ? r : kout(r)]), r >= h2 ? ry : rz,
+                                                      8 * t, 2048 * r, 2);
+        }
+    };
+
+    const int tick_cap = 4 * cnt + 32;  // a stale counter can only end the loop early, never hang it
+    int tick = 0;
+    auto end_tick = [&]() -> bool {
+        trio_barrier();
+        bool live = false;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (ph[s] == 3) {  // slot s finished its segment: the next one becomes current
+                cur[s] = nxt[s];
+                nxt[s] = nxt[s] < cnt ? __builtin_amdgcn_readfirstlane(sh.nidx[s]) : cnt;
+            }
+            ph[s] = ph[s] < 0 ? (tick + 1 == s ? 2 : -1) : (ph[s] == 3 ? 0 : ph[s] + 1);
+            live = live || ph[s] < 0 || cur[s] < cnt || nxt[s] < cnt;
+        }
+        ++tick;
+        return live && tick < tick_cap;
+    };
+    bool go = true;
+    for (int i = 0; i < slot && go; ++i) go = end_tick();
+    while (go) {
+        stage2();
+        if (!(go = end_tick())) break;
+        stage3();
+        if (!(go = end_tick())) break;
+        stage0();
+        if (!(go = end_tick())) break;
+        stage1();
+        go = end_tick();
+    }
+}
+
 static int g_lab_variant = 0, g_lab_lds = 0, g_lab_tok = 0;
 extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int lds, int tok) {
     g_lab_variant = v;
@@ -583,6 +970,46 @@ hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n,
     const long long q = (hi - lo + 7) / 8;
     const dim3 grid((unsigned)(8 * q), (unsigned)channels);
 #ifdef SDSP_OLS_LAB
+    if (g_lab_variant >= 1028 && g_lab_variant < 1031) {  // quad kernel (+ ablation)
+        static int par = 0;
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        const int J = g_lab_lds > 0 ? g_lab_lds : cus / 8;
+        if (channels != 1) return hipErrorInvalidValue;
+        const dim3 g4(8 * J);
+        const int abl = g_lab_variant - 1028;
+        if (abl == 0)
+            hipLaunchKernelGGL(fir_ols_quad_kernel<0>, g4, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        else if (abl == 1)
+            hipLaunchKernelGGL(fir_ols_quad_kernel<1>, g4, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        else
+            hipLaunchKernelGGL(fir_ols_quad_kernel<2>, g4, dim3(1024), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        par ^= 1;
+        return hipGetLastError();
+    }
+    if (g_lab_variant >= 1024 && g_lab_variant < 1027) {  // trio kernel (+ ablation)
+        static int par = 0;
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        const int J = g_lab_lds > 0 ? g_lab_lds : cus / 8;
+        if (channels != 1) return hipErrorInvalidValue;
+        const dim3 g3(8 * J);
+        const int abl = g_lab_variant - 1024;
+        if (abl == 0)
+            hipLaunchKernelGGL(fir_ols_trio_kernel<0>, g3, dim3(768), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        else if (abl == 1)
+            hipLaunchKernelGGL(fir_ols_trio_kernel<1>, g3, dim3(768), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        else
+            hipLaunchKernelGGL(fir_ols_trio_kernel<2>, g3, dim3(768), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        par ^= 1;
+        return hipGetLastError();
+    }
     if (g_lab_variant == 512) {  // staggered pair kernel
         const long long q2 = (q + 1) / 2;
         hipLaunchKernelGGL(fir_ols_pair_kernel<0>, dim3((unsigned)(8 * q2), (unsigned)channels), dim3(512), 0, s,
