@@ -381,9 +381,9 @@ class Cfg5Chan:
         self.samples_per_step = self.S * self.n
         self.bytes_per_step = 16 * self.S * self.n
         self.dtype = "c32 (f32 taps x complex-f32 samples)"
-        self.kernel = ("chan1024_kernel<8, 1024, prefetch> (streaming PFB in registers, next round's samples "
-                       "requested before this round's stores, packed-FP32 16x16x4 FFT with one swizzled LDS "
-                       "transpose and a row-swap DFT4)")
+        self.kernel = ("chan1024_kernel<8, 1024, prefetch, 8> (streaming PFB in registers, rounds of 8 frames, "
+                       "next round's samples requested before this round's stores, packed-FP32 16x16x4 FFT with "
+                       "one swizzled LDS transpose and a row-swap DFT4)")
         self.workload = "cfg5: 1024-channel PFB (K=8) + 1024-pt FFT, 8 streams x 2^24 samples per GPU"
         self.algo_name = "chan"
 

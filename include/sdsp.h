@@ -135,10 +135,12 @@ typedef enum {
     SDSP_TUNE_DECIM_SEG = 6,     /* FMA decimator: outputs per lane group (0 = automatic) */
     SDSP_TUNE_IIR_WAVE_SCAN = 7, /* IIR scan kernel: 0 = block scan, 1 (default) = wave scan with 256-byte chunks,
                                     2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */
-    SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: streaming M=1024 kernel where it applies: 3 (default) =
-                                     1024-thread workgroups, next round's samples requested before this
-                                     round's stores; 1 = the same without; 2 / 4 = 512-thread workgroups
-                                     without / with that prefetch; 0 = per-frame kernel */
+    SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: streaming M=1024 kernel where it applies: 3 = 1024-thread
+                                     workgroups, sixteen frames per round, the next round's samples
+                                     requested before this round's stores; 1 = the same without; 2 / 4 =
+                                     512-thread workgroups without / with that prefetch; 5 (default) / 6 =
+                                     as 3 with eight / four frames per round (waves 0..7 / 0..3 transform);
+                                     0 = per-frame kernel */
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
     SDSP_TUNE_OLS_KERNEL = 14,   /* overlap-save interior segments (16-byte aligned rows): 0 (default) one-shot
                                     XCD-ordered kernel, 1 persistent packed kernel (L <= 1025), 2 scalar kernel */

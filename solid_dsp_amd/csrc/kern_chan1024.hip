@@ -270,12 +270,20 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // vmcnt counts loads and stores in issue order, so loads issued after the
 // stores would make every round wait for the previous round's stores
 // (cfg5: 0.423 -> 0.414 ms against the 512-thread form, 25-round A/B).
-template <int K, int T, bool PF>
+// R (frames per round) defaults to one per wave; R = 8 / 4 with T = 1024 (SDSP_TUNE_CHAN_STREAMING
+// = 5 / 6) halve / quarter the bytes a CU has in flight per round (R x 8 KB of loads and as
+// many of stores) and transform the round's frames on waves 0..R-1.
+template <int K, int T, bool PF, int R = T / 64>
 __global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD: 128 VGPRs
 chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
                 f2* __restrict__ y, const f2* __restrict__ tw, long long n, long long frames, int F, int cps,
                 int C, int xcd) {
-    constexpr int kThreads = T, kNB = kM / T, kFrames = T / 64;
+    constexpr int kThreads = T, kNB = kM / T, kFrames = R;
+    static_assert(R <= T / 64, "one frame per wave at most");
+    // the PFB ring holds the last 8 inputs of a branch, slot = frame mod 8: rounds of fewer
+    // than 8 frames run as 8 / R sub-rounds of one 8-frame step (compile-time slots)
+    constexpr int kStep = R < 8 ? 8 : R;
+    static_assert(kStep % 8 == 0 && kStep % R == 0, "ring slots are frame mod 8");
     __shared__ ChanTw stw;
     __shared__ f2 sbuf[kFrames * kM];
     const int t = threadIdx.x, L = t & 63, w = t >> 6;
@@ -301,7 +309,6 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
     const unsigned c_lo = xcd ? (bid & 7) * Q : 0, c_hi = c_lo + Q < (unsigned)C ? c_lo + Q : C;
     const unsigned c_first = c_lo + (xcd ? bid >> 3 : bid);
     const long long H = (long long)(K - 1) * kM;
-    static_assert(kFrames % 8 == 0, "ring slots are frame mod 8");
     const f2* __restrict__ xs = x;
     const f2* __restrict__ hs = hist;
     f2* __restrict__ ys = y;
@@ -405,41 +412,48 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
         // so waiting for them (vmcnt counts loads and stores in issue order) never
         // waits for the stores
         if (PF) load_round(m0);
-        for (long long mb = m0; mb < m_end; mb += kFrames) {
+        for (long long mb = m0; mb < m_end; mb += kStep) {
             load_taps();
-            if (!PF) load_round(mb);
-            // PFB: frame mb + g into buffer g (ring slot g mod 8); per component
-            // acc = fma(c_i, h, acc), one v_pk_fma_f32 per tap
 #pragma unroll
-            for (int g = 0; g < kFrames; ++g) {
-                f2 pacc[kNB];
+            for (int sub = 0; sub < kStep / kFrames; ++sub) {
+                const long long mr = mb + (long long)sub * kFrames;
+                if (mr >= m_end) break;  // uniform
+                if (!PF) load_round(mr);
+                // PFB: frame mr + g into buffer g (ring slot (sub R + g) mod 8); per component
+                // acc = fma(c_i, h, acc), one v_pk_fma_f32 per tap
 #pragma unroll
-                for (int j = 0; j < kNB; ++j) {
-                    ring[j][g & 7] = nx[g][j];
-                    f2 acc = {0.0f, 0.0f};
+                for (int g = 0; g < kFrames; ++g) {
+                    const int sl = sub * kFrames + g;
+                    f2 pacc[kNB];
 #pragma unroll
-                    for (int i = 0; i < K; ++i)
-                        acc = __builtin_elementwise_fma(f2{c[j][i], c[j][i]}, ring[j][(g - i) & 7], acc);
-                    pacc[j] = acc;
+                    for (int j = 0; j < kNB; ++j) {
+                        ring[j][sl & 7] = nx[g][j];
+                        f2 acc = {0.0f, 0.0f};
+#pragma unroll
+                        for (int i = 0; i < K; ++i)
+                            acc = __builtin_elementwise_fma(f2{c[j][i], c[j][i]}, ring[j][(sl - i) & 7], acc);
+                        pacc[j] = acc;
+                    }
+                    if constexpr (kPair) {  // branches 2t, 2t+1: one 16-byte LDS store
+                        *reinterpret_cast<pk::f4v*>(sbuf + g * kM + 2 * t) = pk::f4v{pacc[0].x, pacc[0].y, pacc[1].x, pacc[1].y};
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < kNB; ++j) sbuf[g * kM + t + kThreads * j] = pacc[j];
+                    }
                 }
-                if constexpr (kPair) {  // branches 2t, 2t+1: one 16-byte LDS store
-                    *reinterpret_cast<pk::f4v*>(sbuf + g * kM + 2 * t) = pk::f4v{pacc[0].x, pacc[0].y, pacc[1].x, pacc[1].y};
+                if (PF && mr + kFrames < m_end) load_round(mr + kFrames);
+                __syncthreads();
+                const long long f = mr + w;
+                if (w >= kFrames) {  // uniform per wave: no frame for this wave in the round
+                } else if (lab & 1) {
+                    if (!(lab & 4) && f < m_end)
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) st_nt2(ys + f * kM + L + 64 * k, sbuf[w * kM + L + 64 * k]);
                 } else {
-#pragma unroll
-                    for (int j = 0; j < kNB; ++j) sbuf[g * kM + t + kThreads * j] = pacc[j];
+                    fft1024_chan(sbuf + w * kM, stw, L, ys + f * kM, f < m_end && !(lab & 4));
                 }
+                __syncthreads();
             }
-            if (PF && mb + kFrames < m_end) load_round(mb + kFrames);
-            __syncthreads();
-            const long long f = mb + w;
-            if (lab & 1) {
-                if (!(lab & 4) && f < m_end)
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) st_nt2(ys + f * kM + L + 64 * k, sbuf[w * kM + L + 64 * k]);
-            } else {
-                fft1024_chan(sbuf + w * kM, stw, L, ys + f * kM, f < m_end && !(lab & 4));
-            }
-            __syncthreads();
         }
     }
 }
@@ -641,7 +655,7 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
     const int var = (a.fast == 2 || a.fast == 4) && ((uintptr_t)a.x & 15) ? 1 : a.fast;
     // chunk of F frames (a whole number of rounds); each chunk re-reads K-1 warm-up
     // frames (L2 hits when the neighbouring chunk is in flight on the same XCD)
-    const int R = var == 2 || var == 4 ? 8 : 16;  // frames per round
+    const int R = var == 2 || var == 4 || var == 5 || var == 6 ? 8 : 16;  // frames per step (chunks: whole steps)
     long long Fd = (long long)(a.frames * a.streams) / 512;
     Fd = Fd < 64 ? 64 : (Fd > 256 ? 256 : Fd);
     const int F = (int)(((a.frames_per_block > 0 ? a.frames_per_block : Fd) + R - 1) / R * R);
@@ -659,8 +673,8 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
 #ifdef SDSP_CHAN_LAB
     xcd |= g_chan_lab << 4;
 #endif
-#define SDSP_CHAN_T(KV, T, PF)                                                                             \
-    hipLaunchKernelGGL((chan1024_kernel<KV, T, PF>), grid, dim3(T), 0, s, (const f2*)a.x, (const f2*)a.hist,     \
+#define SDSP_CHAN_T(KV, T, PF, ...)                                                                        \
+    hipLaunchKernelGGL((chan1024_kernel<KV, T, PF, ##__VA_ARGS__>), grid, dim3(T), 0, s, (const f2*)a.x, (const f2*)a.hist,     \
                        (const float*)a.cb, (f2*)a.y, (const f2*)a.tw, (long long)a.n, (long long)a.frames, F, (int)cps, \
                        (int)C, xcd)
 #define SDSP_CHAN(KV)                                                                      \
@@ -668,6 +682,8 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
         if (var == 2) SDSP_CHAN_T(KV, 512, false);                                         \
         else if (var == 3) SDSP_CHAN_T(KV, 1024, true);                                    \
         else if (var == 4) SDSP_CHAN_T(KV, 512, true);                                     \
+        else if (var == 5) SDSP_CHAN_T(KV, 1024, true, 8);                                 \
+        else if (var == 6) SDSP_CHAN_T(KV, 1024, true, 4);                                 \
         else SDSP_CHAN_T(KV, 1024, false);                 \
         break;
     switch (a.K) {

@@ -192,7 +192,7 @@ struct sdsp_chan {
     std::vector<unsigned char> taps;
     DevBuf cb, tw, hist[2], stage_in, stage_out;
     int cur = 0;
-    int fast = 3;  // streaming M = 1024 kernel variant (SDSP_TUNE_CHAN_STREAMING)
+    int fast = 5;  // streaming M = 1024 kernel variant (SDSP_TUNE_CHAN_STREAMING): 8-frame rounds
     int fpb = 0;       // its frames per workgroup (SDSP_TUNE_CHAN_FRAMES_PER_BLOCK, 0 = default)
     bool xcd = true;   // XCD-contiguous chunk order (SDSP_TUNE_CHAN_XCD_ORDER)
     hipStream_t stream = nullptr;
@@ -404,7 +404,7 @@ int sdsp_chan_set_streams(sdsp_chan* h, size_t streams) {
 
 int sdsp_chan_set_tuning(sdsp_chan* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
-    if (key == SDSP_TUNE_CHAN_STREAMING && value >= 0 && value <= 4) h->fast = value;
+    if (key == SDSP_TUNE_CHAN_STREAMING && value >= 0 && value <= 6) h->fast = value;
     else if (key == SDSP_TUNE_CHAN_FRAMES_PER_BLOCK && value >= 0) h->fpb = value;
     else if (key == SDSP_TUNE_CHAN_XCD_ORDER) h->xcd = value != 0;
     else return SDSP_E_INVALID_ARGUMENT;

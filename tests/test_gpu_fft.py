@@ -102,12 +102,13 @@ def test_channelizer_multistream_device():
         assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-7
 
 
-@pytest.mark.parametrize("variant,fpb", [(0, 0), (1, 16), (1, 0), (2, 8), (2, 48), (3, 16), (3, 0), (4, 8), (4, 48)])
+@pytest.mark.parametrize("variant,fpb", [(0, 0), (1, 16), (1, 0), (2, 8), (2, 48), (3, 16), (3, 0), (4, 8), (4, 48),
+                                         (5, 8), (5, 0), (6, 8), (6, 0)])
 @pytest.mark.parametrize("K", [3, 8])
 @pytest.mark.parametrize("xcd", [0, 1])
 def test_channelizer_1024_streaming_variants(variant, fpb, K, xcd):
     """the streaming M=1024 kernels (1024- and 512-thread workgroups, SDSP_TUNE_CHAN_STREAMING
-    1/2) and the per-frame kernel (0) against the restatement: several streams, workgroup
+    1-4; 5 / 6: eight / four frames per round) and the per-frame kernel (0) against the restatement: several streams, workgroup
     boundaries inside a block (warm-up frames), a ragged last round, two blocks (history),
     launch-order and XCD-ordered chunk maps"""
     import torch
@@ -132,7 +133,7 @@ def test_channelizer_1024_streaming_variants(variant, fpb, K, xcd):
         assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-6
 
 
-@pytest.mark.parametrize("variant,fpb", [(1, 16), (2, 8), (3, 16), (4, 8)])
+@pytest.mark.parametrize("variant,fpb", [(1, 16), (2, 8), (3, 16), (4, 8), (5, 8), (6, 8)])
 @pytest.mark.parametrize("xcd", [0, 1])
 def test_channelizer_1024_persistent_chunk_walk(variant, fpb, xcd):
     """more chunks than resident workgroups: every workgroup walks several chunks
