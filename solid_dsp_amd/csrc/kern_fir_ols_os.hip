@@ -941,6 +941,163 @@ fir_ols_quad_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, con
     }
 }
 
+// Queue kernel (lab): persistent 256-lane workgroups, three per CU, each running the
+// one-shot kernel's segment transform (bit-identical) on a queue of segments with the
+// next segment's loads in flight across the current one's P2-P5 (issued right after
+// P1, into registers) -- no coupling between workgroups, so each CU's compute stays
+// free-running, while a segment's loads are outstanding only for their latency rather
+// than for a whole workgroup lifetime.  Segments from a per-XCD-eighth counter (one
+// returning atomic per segment, issued before the loads so that waiting for it never
+// waits for them); the index is published in LDS before the P4 -> P5 barrier.
+__device__ unsigned int g_ols_queue_q[2][8 * 32];
+
+template <int ABL>
+__global__ void __launch_bounds__(256, 3)
+fir_ols_queue_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
+                     f2* __restrict__ y, long long lo, long long hi, long long q, int h2, int par) {
+    __shared__ __attribute__((aligned(16))) f2 img[16 * kRow];
+    __shared__ int nidx;
+    const int t = threadIdx.x, hi4 = t >> 4, lo4 = t & 15;
+    const int xc = blockIdx.x & 7, J = gridDim.x >> 3, jb = blockIdx.x >> 3;
+    const long long s0 = lo + (long long)xc * q, se0 = s0 + q, se = se0 < hi ? se0 : hi;
+    const int cnt = se > s0 ? (int)(se - s0) : 0;
+    const int V = 4096 - 256 * h2;
+    unsigned int* ctr = &g_ols_queue_q[par][32 * xc];
+    if (blockIdx.x == 0 && t < 8)  // the next launch's counters (the previous launch used them)
+        __hip_atomic_store(&g_ols_queue_q[par ^ 1][32 * t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
+    const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0, 2048 * 16, kBufWord3);
+    const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 0, kBufWord3);
+    auto seg_rsrc = [&](const f2* base, int k) {  // none past the eighth: loads return 0, stores drop
+        const bool ok = (unsigned)k < (unsigned)cnt;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (s0 + (ok ? k : 0)) * V - 256 * h2), (short)0,
+                                                 ok ? 32768 : 0, kBufWord3);
+    };
+    auto next_index = [&](unsigned got) -> int {  // dynamic indices follow the static first round
+        return got < (unsigned)cnt ? (int)min((unsigned)cnt, (unsigned)J + got) : cnt;
+    };
+    const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 0, 0));
+    const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 4096, 0));
+    const float4 b2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 8192, 0));
+    f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
+    f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
+    f2* col = img + t + (t >> 4);
+    f2* r2 = img + hi4 * kRow + lo4;
+    f2* r3 = img + hi4 * kRow + 17 * lo4;
+
+    int k = jb < cnt ? jb : cnt;  // uniform
+    if (k >= cnt) return;
+    unsigned got = 0;
+    if (t == 0) got = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f2 v[16], vn[16];
+    {
+        const auto rx = seg_rsrc(x, k);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            if constexpr (ABL == 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)k};
+            else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+        }
+    }
+    // 16 dropped stores (empty descriptor): the loop is entered with 16 memory operations younger
+    // than the segment's loads on every path, so P1's wait for them is vmcnt(16) on both
+#pragma unroll
+    for (int r = 0; r < 16; ++r) __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rz, 8 * t, 2048 * r, 0);
+    if (t == 0) nidx = next_index(got);
+    trio_barrier();
+    int kn = __builtin_amdgcn_readfirstlane(nidx);
+    for (int it = 0; it <= cnt; ++it) {  // bounded: one segment per iteration
+        // P1: DFT16 n2 -> k0, * W4096^(t k0) -> (k0, t)
+        if constexpr (ABL != 1) {
+            pdft16<false>(v);
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) col[kk * kRow] = kk == 0 ? v[0] : pmul(v[kout(kk)], tw_pair(Cb, Da, kk));
+        }
+        // P2/P3's tables, the queue index of the segment after the next, then the next segment's
+        // loads -- in this order, so that waiting for the tables or the index never waits for them
+        float4 hq[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+        const float4 e0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12288, 0));
+        const float4 e1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12544, 0));
+        const float4 e2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12800, 0));
+        if (t == 0 && kn < cnt) got = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        {
+            const auto rx = seg_rsrc(x, kn);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                if constexpr (ABL == 2) vn[r] = f2{1e-3f * t + r, 1e-9f * (float)kn};
+                else vn[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+            }
+        }
+        if constexpr (ABL != 1) {
+            trio_barrier();
+            // P2: lane (k0 = hi4, n0 = lo4): DFT16 n1 -> k1, * W256^(n0 k1)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
+            const f2 Eb[3] = {f2{e0.x, e0.y}, f2{e0.z, e0.w}, f2{e1.x, e1.y}};
+            const f2 Fa[3] = {f2{e1.z, e1.w}, f2{e2.x, e2.y}, f2{e2.z, e2.w}};
+            f2 w2[16];
+#pragma unroll
+            for (int kk = 1; kk < 16; ++kk) w2[kk] = tw_pair(Eb, Fa, kk);
+            pdft16<false>(v);
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) r2[17 * kk] = kk == 0 ? v[0] : pmul(v[kout(kk)], w2[kk]);
+            phase_sync<true>();
+            // P3: DFT16 n0 -> k2, * H, IDFT16 k2 -> n0, * conj W256^(k1 n0)
+            {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[j] = r3[j];
+                pdft16<false>(v);
+                f2 u[16];
+#pragma unroll
+                for (int p = 0; p < 8; ++p) {
+                    u[2 * p] = pmul(v[kout(2 * p)], f2{hq[p].x, hq[p].y});
+                    u[2 * p + 1] = pmul(v[kout(2 * p + 1)], f2{hq[p].z, hq[p].w});
+                }
+                pdft16<true>(u);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) r3[j] = j == 0 ? u[kout(0)] : pmulc(u[kout(j)], w2[j]);
+            }
+            phase_sync<true>();
+            // P4: IDFT16 k1 -> n1
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
+            pdft16<true>(v);
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) r2[17 * kk] = v[kout(kk)];
+        }
+        if (t == 0) nidx = kn < cnt ? next_index(got) : cnt;  // read after the barrier below
+        trio_barrier();
+        const int knn = __builtin_amdgcn_readfirstlane(nidx);
+        // P5: * conj W4096^(t k0), IDFT16 k0 -> n2, and the stores
+        const auto ry = seg_rsrc(y, k);
+        if constexpr (ABL != 1) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Cb[i]), "+v"(Da[i]));
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) v[kk] = kk == 0 ? col[0] : pmulc(col[kk * kRow], tw_pair(Cb, Da, kk));
+            pdft16<true>(v);
+        }
+        if constexpr (ABL == 2) {
+            f2 acc = v[0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) acc += v[r];
+            if (acc.x == 1.2345e30f) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc), ry, 8 * t, 0, 0);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[ABL == 1 ? r : kout(r)]), r >= h2 ? ry : rz,
+                                                      8 * t, 2048 * r, 2);
+        }
+        if (kn >= cnt) break;  // uniform
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = vn[r];
+        k = kn;
+        kn = knn;
+        // P1 of the next segment rewrites the columns P5 just read: lane-owned, no barrier
+    }
+}
+
 static int g_lab_variant = 0, g_lab_lds = 0, g_lab_tok = 0;
 extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int lds, int tok) {
     g_lab_variant = v;
@@ -970,6 +1127,26 @@ hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n,
     const long long q = (hi - lo + 7) / 8;
     const dim3 grid((unsigned)(8 * q), (unsigned)channels);
 #ifdef SDSP_OLS_LAB
+    if (g_lab_variant >= 2048 && g_lab_variant < 2051) {  // queue kernel (+ ablation); lds field = workgroups per XCD
+        static int par = 0;
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+        const int J = g_lab_lds > 0 ? g_lab_lds : 3 * cus / 8;
+        if (channels != 1) return hipErrorInvalidValue;
+        const dim3 gq(8 * J);
+        const int abl = g_lab_variant - 2048;
+        if (abl == 0)
+            hipLaunchKernelGGL(fir_ols_queue_kernel<0>, gq, dim3(256), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        else if (abl == 1)
+            hipLaunchKernelGGL(fir_ols_queue_kernel<1>, gq, dim3(256), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        else
+            hipLaunchKernelGGL(fir_ols_queue_kernel<2>, gq, dim3(256), 0, s, (const f2*)x, (const float4*)p.d_pkt,
+                               (const float4*)p.d_ostab, (f2*)y, lo, hi, q, p.halo_rows, par);
+        par ^= 1;
+        return hipGetLastError();
+    }
     if (g_lab_variant >= 1028 && g_lab_variant < 1031) {  // quad kernel (+ ablation)
         static int par = 0;
         int cus = 256;
