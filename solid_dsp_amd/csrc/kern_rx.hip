@@ -31,6 +31,7 @@
 // stages kAgcS samples of each through LDS so that HBM sees 16 * kAgcS-byte
 // runs per channel instead of one sample per lane per row.
 #include "sdsp.h"
+#include <cstdlib>
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 
@@ -62,10 +63,17 @@ __device__ inline cpx<T> ext_at(const cpx<T>* __restrict__ x, const cpx<T>* __re
 // downward, reads each p once from LDS and adds it to every accumulator whose
 // jj = r - q lies in [0, cj) — the same additions in the same order as the
 // one-output-per-lane form, with kR-fold fewer LDS reads.
-template <typename T>
+// STAGE (delays d <= kDmax): the chunk's input x[base - d, base + cnt) is staged in LDS
+// once and each product reads both of its factors there (one load per input sample
+// instead of two, 16 fewer VGPRs per load slot); otherwise both factors are loaded.
+constexpr int kDmax = 256;
+template <typename T, bool STAGE>
 __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__ x, const cpx<T>* __restrict__ hist,
                                                       cpx<T>* __restrict__ y, long long n, int H, int d, int K) {
-    __shared__ cpx<T> p[pad8(kOut + kChunk - 1) + 1];
+    // LDS sized by the launch (acorr_lds_bytes): p for the widest chunk, then (STAGE) the staged input
+    extern __shared__ __attribute__((aligned(16))) char acorr_lds[];
+    cpx<T>* p = reinterpret_cast<cpx<T>*>(acorr_lds);
+    cpx<T>* xs = p + pad8(kOut + (K < kChunk ? K : kChunk) - 1) + 1;
     const int ch = blockIdx.y;
     x += (long long)ch * n;
     y += (long long)ch * n;
@@ -84,6 +92,36 @@ __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__
         // every load of the chunk is issued before the first product: the loads of
         // one lane are independent, so the wave keeps kLd x 2 requests in flight
         constexpr int kLd = (kOut + kChunk - 1 + kTile - 1) / kTile;
+        if constexpr (STAGE) {
+            constexpr int kLs = (kOut + kChunk - 1 + kDmax + kTile - 1) / kTile;
+            const long long b0 = base - d;  // xs[i] = x[b0 + i], i < cnt + d
+            const int ns = cnt + d;
+            cpx<T> v[kLs];
+            if (b0 >= 0 && base + cnt <= n) {  // interior tile: plain loads
+#pragma unroll
+                for (int k = 0; k < kLs; ++k) {
+                    const int i = t + k * kTile;
+                    if (i < ns) v[k] = x[b0 + i];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < kLs; ++k) {
+                    const int i = t + k * kTile;
+                    if (i < ns) v[k] = ext_at(x, hist, b0 + i, H);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kLs; ++k) {
+                const int i = t + k * kTile;
+                if (i < ns) xs[i] = v[k];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kLd; ++k) {
+                const int s = t + k * kTile;
+                if (s < cnt) p[pad8(s)] = mul_(xs[s + d], conj_(xs[s]));
+            }
+        } else {
         cpx<T> va[kLd], vb[kLd];
         if (base - d >= 0 && base + cnt <= n) {  // interior tile: plain loads
 #pragma unroll
@@ -108,6 +146,7 @@ __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__
         for (int k = 0; k < kLd; ++k) {
             const int s = t + k * kTile;
             if (s < cnt) p[pad8(s)] = mul_(va[k], conj_(vb[k]));
+        }
         }
         __syncthreads();
         // slot of p[n0 + kR t + q - j0] is kR t + q + cj - 1
@@ -352,16 +391,35 @@ __global__ void __launch_bounds__(64) agc_init_kernel(const AgcSample<CPLX>* __r
 
 }  // namespace
 
+// dynamic LDS of acorr_kernel: the product tile of the widest chunk, plus the staged input
+static size_t acorr_lds_bytes(size_t elem, int d, int K, bool stage) {
+    const int cj = K < kChunk ? K : kChunk;
+    const size_t np = (size_t)pad8(kOut + cj - 1) + 1, nx = stage ? (size_t)(kOut + cj - 1 + d) : 0;
+    return (np + nx) * elem;
+}
+
 hipError_t launch_acorr(int prec, const void* x, const void* hist, void* y, size_t n, int H, int d, int K,
                         size_t channels, hipStream_t s) {
     if (n == 0) return hipSuccess;
     dim3 grid((unsigned)((n + kOut - 1) / kOut), (unsigned)channels);
-    if (prec == 0)
-        hipLaunchKernelGGL(acorr_kernel<float>, grid, dim3(kTile), 0, s, (const c32*)x, (const c32*)hist, (c32*)y,
-                           (long long)n, H, d, K);
-    else
-        hipLaunchKernelGGL(acorr_kernel<double>, grid, dim3(kTile), 0, s, (const c64*)x, (const c64*)hist, (c64*)y,
-                           (long long)n, H, d, K);
+    static const bool nostage = std::getenv("SDSP_ACORR_NOSTAGE") != nullptr;  // A/B switch
+    const bool stage = d <= kDmax && !nostage;
+    const size_t lds = acorr_lds_bytes(prec == 0 ? sizeof(c32) : sizeof(c64), d, K, stage);
+    if (prec == 0) {
+        if (stage)
+            hipLaunchKernelGGL((acorr_kernel<float, true>), grid, dim3(kTile), lds, s, (const c32*)x, (const c32*)hist,
+                               (c32*)y, (long long)n, H, d, K);
+        else
+            hipLaunchKernelGGL((acorr_kernel<float, false>), grid, dim3(kTile), lds, s, (const c32*)x, (const c32*)hist,
+                               (c32*)y, (long long)n, H, d, K);
+    } else {
+        if (stage)
+            hipLaunchKernelGGL((acorr_kernel<double, true>), grid, dim3(kTile), lds, s, (const c64*)x, (const c64*)hist,
+                               (c64*)y, (long long)n, H, d, K);
+        else
+            hipLaunchKernelGGL((acorr_kernel<double, false>), grid, dim3(kTile), lds, s, (const c64*)x, (const c64*)hist,
+                               (c64*)y, (long long)n, H, d, K);
+    }
     return hipGetLastError();
 }
 
