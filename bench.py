@@ -485,7 +485,8 @@ class Cfg6ACorr:
         self.samples_per_step = self.n
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (complex-f32 products and sums, f64 energy)"
-        self.kernel = "acorr_kernel<float> (LDS-staged conj products, one-wave workgroups of 512 outputs, 8 per lane) + energy + history"
+        self.kernel = ("acorr_pipe_kernel<float> (persistent one-wave workgroups over tiles of 512 outputs, 8 per lane, the "
+                       "next tile's inputs loaded across this tile's sums; LDS-staged conj products) + edge tiles + energy + history")
         self.parity_check = "bit mismatches vs the c32 restatement over the first 2^20 outputs (must be 0)"
         self.workload = f"cfg6: AutoCorrelator(64, 16), c32, 2^{int(np.log2(self.n))} samples per channel"
         self.algo_name = "acorr"

@@ -69,7 +69,8 @@ __device__ inline cpx<T> ext_at(const cpx<T>* __restrict__ x, const cpx<T>* __re
 constexpr int kDmax = 256;
 template <typename T, bool STAGE>
 __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__ x, const cpx<T>* __restrict__ hist,
-                                                      cpx<T>* __restrict__ y, long long n, int H, int d, int K) {
+                                                      cpx<T>* __restrict__ y, long long n, int H, int d, int K,
+                                                      long long tile0) {
     // LDS sized by the launch (acorr_lds_bytes): p for the widest chunk, then (STAGE) the staged input
     extern __shared__ __attribute__((aligned(16))) char acorr_lds[];
     cpx<T>* p = reinterpret_cast<cpx<T>*>(acorr_lds);
@@ -79,7 +80,7 @@ __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__
     y += (long long)ch * n;
     hist += (long long)ch * H;
     const int t = threadIdx.x;
-    const long long n0 = (long long)xcd_order(blockIdx.x, gridDim.x) * kOut;
+    const long long n0 = (tile0 + (long long)xcd_order(blockIdx.x, gridDim.x)) * kOut;
     cpx<T> acc[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) acc[r] = zero_v<cpx<T>>();
@@ -189,6 +190,119 @@ __global__ void __launch_bounds__(kTile) acorr_kernel(const cpx<T>* __restrict__
     __syncthreads();
     for (int s = t; s < kOut; s += kTile)
         if (n0 + s < n) store_nt(y + n0 + s, p[pad8(s)]);
+}
+
+// Persistent, software-pipelined form (K <= kPipeK, d <= kPipeD; c32 / c64): one
+// wave walks tiles b, b + G, ... of its channel; the next tile's inputs are loaded
+// into registers before this tile's products, sums and stores, so the loads' latency
+// overlaps the 48-add chains instead of stalling each one-shot wave.  Same products,
+// same summation order per output as acorr_kernel (bit-identical).
+constexpr int kPipeK = 128, kPipeD = 128;
+template <typename T>
+__global__ void __launch_bounds__(kTile) acorr_pipe_kernel(const cpx<T>* __restrict__ x, cpx<T>* __restrict__ y,
+                                                           long long n, int d, int K, long long t_lo, long long t_hi) {
+    extern __shared__ __attribute__((aligned(16))) char acorr_lds[];
+    cpx<T>* p = reinterpret_cast<cpx<T>*>(acorr_lds);
+    cpx<T>* xs = p + pad8(kOut + K - 1) + 1;
+    constexpr int kLp = (kOut + kPipeK - 1 + kPipeD + kTile - 1) / kTile;
+    constexpr int kE = (int)sizeof(cpx<T>);
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    const int ch = blockIdx.y;
+    x += (long long)ch * n;
+    y += (long long)ch * n;
+    const int t = threadIdx.x;
+    const int cnt = kOut + K - 1, ns = cnt + d;  // products and staged inputs per tile
+    // one wave per workgroup: LDS hand-offs need only this wave's LDS operations done
+    auto lds_sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    // XCD-ordered walk (gridDim.x a multiple of 8): workgroup b on XCD b % 8 takes tiles
+    // (b / 8) + i G/8 of that XCD's contiguous eighth, so the tiles an XCD has in flight are
+    // neighbours and each tile's K - 1 + d halo samples were just read into the same L2
+    const long long nt = t_hi - t_lo, Q = (nt + 7) / 8, Gx = gridDim.x / 8;
+    const long long e_lo = t_lo + (long long)(blockIdx.x & 7) * Q, e_hi0 = e_lo + Q;
+    const long long e_hi = e_hi0 < t_hi ? e_hi0 : t_hi;
+    long long tile = e_lo + (blockIdx.x >> 3);
+    if (tile >= e_hi) return;
+    cpx<T> v[kLp];
+    // interior tiles only (t_lo..t_hi): x[b0, b0 + ns) lies inside the call; the descriptor's
+    // bound returns zeros past ns, so every lane issues the same kLp loads (no branches)
+    auto load = [&](long long tl) {
+        const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + tl * kOut - (K - 1) - d), (short)0, ns * kE,
+                                                          0x00020000);
+#pragma unroll
+        for (int k = 0; k < kLp; ++k) {
+            if constexpr (kE == 8)
+                v[k] = __builtin_bit_cast(cpx<T>, __builtin_amdgcn_raw_buffer_load_b64(rx, (t + k * kTile) * kE, 0, 0));
+            else
+                v[k] = __builtin_bit_cast(cpx<T>, __builtin_amdgcn_raw_buffer_load_b128(rx, (t + k * kTile) * kE, 0, 0));
+        }
+    };
+    load(tile);
+    for (;;) {
+        const long long n0 = tile * kOut;
+#pragma unroll
+        for (int k = 0; k < kLp; ++k) {
+            const int i = t + k * kTile;
+            if (i < ns) xs[i] = v[k];
+        }
+        lds_sync();
+        const long long nxt = tile + Gx;
+        if (nxt < e_hi) load(nxt);  // in flight across this tile's products, sums and stores
+#pragma unroll
+        for (int k = 0; k < (kOut + kPipeK - 1 + kTile - 1) / kTile; ++k) {
+            const int s = t + k * kTile;
+            if (s < cnt) p[pad8(s)] = mul_(xs[s + d], conj_(xs[s]));
+        }
+        lds_sync();
+        cpx<T> acc[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) acc[r] = zero_v<cpx<T>>();
+        // slot of p[n0 + kR t + q] is kR t + q + K - 1 (the one-shot kernel's single chunk)
+        const int s0 = kR * t + K - 1;
+        if (K >= kR) {
+#pragma unroll
+            for (int q = kR - 1; q >= 0; --q) {
+                const cpx<T> pv = p[pad8(s0 + q)];
+#pragma unroll
+                for (int r = q; r < kR; ++r) acc[r] = add_(acc[r], pv);
+            }
+#pragma unroll 4
+            for (int q = -1; q > kR - 1 - K; --q) {
+                const cpx<T> pv = p[pad8(s0 + q)];
+#pragma unroll
+                for (int r = 0; r < kR; ++r) acc[r] = add_(acc[r], pv);
+            }
+#pragma unroll
+            for (int u = 0; u < kR - 1; ++u) {
+                const cpx<T> pv = p[pad8(s0 + kR - 1 - K - u)];
+#pragma unroll
+                for (int r = 0; r < kR - 1 - u; ++r) acc[r] = add_(acc[r], pv);
+            }
+        } else {
+            for (int q = kR - 1; q > -K; --q) {
+                const cpx<T> pv = p[pad8(s0 + q)];
+#pragma unroll
+                for (int r = 0; r < kR; ++r)
+                    if (r - q >= 0 && r - q < K) acc[r] = add_(acc[r], pv);
+            }
+        }
+        lds_sync();
+#pragma unroll
+        for (int r = 0; r < kR; ++r) p[pad8(kR * t + r)] = acc[r];
+        lds_sync();
+        const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + n0), (short)0, kOut * kE, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < kOut / kTile; ++k) {
+            const cpx<T> o = p[pad8(t + k * kTile)];
+            if constexpr (kE == 8)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, o), ry, (t + k * kTile) * kE, 0, 2);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, o), ry, (t + k * kTile) * kE, 0, 2);
+        }
+        if (nxt >= e_hi) break;
+        tile = nxt;
+        lds_sync();  // every read of xs and p done before the next tile is staged
+    }
 }
 
 // execute() on the current window (no push): the output for the newest history sample
@@ -403,22 +517,65 @@ hipError_t launch_acorr(int prec, const void* x, const void* hist, void* y, size
     if (n == 0) return hipSuccess;
     dim3 grid((unsigned)((n + kOut - 1) / kOut), (unsigned)channels);
     static const bool nostage = std::getenv("SDSP_ACORR_NOSTAGE") != nullptr;  // A/B switch
+    static const bool pipe = std::getenv("SDSP_ACORR_NOPIPE") == nullptr;      // A/B switch
+    if (pipe && K >= 1 && K <= kPipeK && d <= kPipeD) {
+        // interior tiles (whole input window and all outputs inside the call) on the pipelined
+        // kernel; the edge tiles on the one-shot kernel
+        const long long ntiles = (long long)((n + kOut - 1) / kOut);
+        const long long t_lo = (K - 1 + d + kOut - 1) / kOut, t_hi = (long long)(n / kOut);
+        if (t_hi > t_lo) {
+            int cus = 256, per_cu = 0;
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+            const size_t elem = prec == 0 ? sizeof(c32) : sizeof(c64);
+            const size_t lds2 = ((size_t)pad8(kOut + K - 1) + 1 + (size_t)(kOut + K - 1 + d)) * elem;
+            // one persistent wave per resident slot (registers / LDS decide how many per CU)
+            if (prec == 0)
+                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, acorr_pipe_kernel<float>, kTile, lds2);
+            else
+                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, acorr_pipe_kernel<double>, kTile, lds2);
+            const long long res = (long long)(per_cu > 0 ? per_cu : 8) * cus;
+            const long long nt = t_hi - t_lo;
+            long long G = nt < res ? nt : res;
+            G = (G + 7) / 8 * 8;  // whole workgroups per XCD (surplus ones find no tile and return)
+            const dim3 g2((unsigned)G, (unsigned)channels);
+            if (prec == 0)
+                hipLaunchKernelGGL((acorr_pipe_kernel<float>), g2, dim3(kTile), lds2, s, (const c32*)x, (c32*)y,
+                                   (long long)n, d, K, t_lo, t_hi);
+            else
+                hipLaunchKernelGGL((acorr_pipe_kernel<double>), g2, dim3(kTile), lds2, s, (const c64*)x, (c64*)y,
+                                   (long long)n, d, K, t_lo, t_hi);
+            const size_t lds = acorr_lds_bytes(prec == 0 ? sizeof(c32) : sizeof(c64), d, K, true);
+            auto edge = [&](long long a, long long b) {
+                if (b <= a) return;
+                const dim3 ge((unsigned)(b - a), (unsigned)channels);
+                if (prec == 0)
+                    hipLaunchKernelGGL((acorr_kernel<float, true>), ge, dim3(kTile), lds, s, (const c32*)x,
+                                       (const c32*)hist, (c32*)y, (long long)n, H, d, K, a);
+                else
+                    hipLaunchKernelGGL((acorr_kernel<double, true>), ge, dim3(kTile), lds, s, (const c64*)x,
+                                       (const c64*)hist, (c64*)y, (long long)n, H, d, K, a);
+            };
+            edge(0, t_lo);
+            edge(t_hi, ntiles);
+            return hipGetLastError();
+        }
+    }
     const bool stage = d <= kDmax && !nostage;
     const size_t lds = acorr_lds_bytes(prec == 0 ? sizeof(c32) : sizeof(c64), d, K, stage);
     if (prec == 0) {
         if (stage)
             hipLaunchKernelGGL((acorr_kernel<float, true>), grid, dim3(kTile), lds, s, (const c32*)x, (const c32*)hist,
-                               (c32*)y, (long long)n, H, d, K);
+                               (c32*)y, (long long)n, H, d, K, 0LL);
         else
             hipLaunchKernelGGL((acorr_kernel<float, false>), grid, dim3(kTile), lds, s, (const c32*)x, (const c32*)hist,
-                               (c32*)y, (long long)n, H, d, K);
+                               (c32*)y, (long long)n, H, d, K, 0LL);
     } else {
         if (stage)
             hipLaunchKernelGGL((acorr_kernel<double, true>), grid, dim3(kTile), lds, s, (const c64*)x, (const c64*)hist,
-                               (c64*)y, (long long)n, H, d, K);
+                               (c64*)y, (long long)n, H, d, K, 0LL);
         else
             hipLaunchKernelGGL((acorr_kernel<double, false>), grid, dim3(kTile), lds, s, (const c64*)x, (const c64*)hist,
-                               (c64*)y, (long long)n, H, d, K);
+                               (c64*)y, (long long)n, H, d, K, 0LL);
     }
     return hipGetLastError();
 }

@@ -75,6 +75,27 @@ def test_acorr_channels_and_device():
     assert np.allclose(e, ref, rtol=1e-6)
 
 
+@pytest.mark.parametrize("w,d,dt", [(64, 16, C64), (130, 120, C64), (64, 16, C128), (9, 0, C64)])
+def test_acorr_pipelined_many_tiles(w, d, dt):
+    """the persistent pipelined kernel (K, d <= 128): more tiles than resident waves, so every
+    wave walks several tiles with the next tile's loads in flight; ragged length, two channels,
+    edge tiles on the one-shot kernel -- bit-identical to the restatement"""
+    import torch
+    import solid_dsp_amd as sd
+    rng = np.random.default_rng(w + d)
+    ch, n = 2, (1 << 22) + 333
+    x = _rand(rng, ch * n, dt).reshape(ch, n)
+    g = sd.AutoCorrelator(w, d, dtype=dt, channels=ch)
+    d_in = torch.from_numpy(x).to("cuda")
+    d_out = torch.empty_like(d_in)
+    g.execute_block_device(d_in, n, d_out, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    y = d_out.cpu().numpy()
+    for c in range(ch):
+        o = O.AutoCorr(w, d, dt)
+        assert y[c].tobytes() == o.execute_block(x[c]).tobytes(), c
+
+
 def test_nco_mix_bit_identical_and_state():
     import solid_dsp_amd as sd
     rng = np.random.default_rng(12)
