@@ -545,7 +545,7 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 // contiguous runs.  Same arithmetic, element order and twiddles as
 // fft1024_pass_kernel<INV, TW, 16> (bit-identical).
 #ifndef SDSP_FFT_PIPE_PRE
-#define SDSP_FFT_PIPE_PRE 16
+#define SDSP_FFT_PIPE_PRE 8
 #endif
 template <bool INV, bool TW, bool CFAST, bool OFAST>
 __global__ void __launch_bounds__(1024)
@@ -581,10 +581,13 @@ fft1024_pipe_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
     const unsigned out_k = (unsigned)(ofast ? 64 * So : T1) * 8u;
     typedef unsigned u2v __attribute__((ext_vector_type(2)));
     cf v[16];
-    auto load = [&](long long grp, int k0, int k1) {
+    // past the last group (ok false): an empty descriptor, so the loads return zeros without touching
+    // memory and every path issues the same loads -- no branch around them, whose merge would make
+    // the compiler wait for all of them at once
+    auto load = [&](long long grp, int k0, int k1, bool ok = true) {
         long long ib, ob, g0;
-        bases(grp, ib, ob, g0);
-        const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + ib), (short)0, 0x7fffffff, 0x00020000);
+        bases(ok ? grp : 0, ib, ob, g0);
+        const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + ib), (short)0, ok ? 0x7fffffff : 0, 0x00020000);
 #pragma unroll
         for (int k = k0; k < k1; ++k)
             v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, 0));
@@ -607,14 +610,17 @@ fft1024_pipe_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
             if (t < TPB * 16) ktab[t] = twx_at(64 * (g0 + (t >> 4)) * (long long)(t & 15));
             if (ofast) tbase = twx_at((g0 + (t & (TPB - 1))) * (long long)(t >> kLog));
         }
+        asm volatile("" : "+v"(tbase.re), "+v"(tbase.im));  // formed here, before the next group's loads
         __syncthreads();
         // the next group's loads: half in flight across this group's FFT, half across its
-        // stores (all sixteen held through the FFT spill registers at 1024 threads)
+        // stores.  Holding more of them through the FFT makes it spill (1024 threads: 128
+        // VGPRs), and every scratch reload waits for all outstanding loads (vmcnt counts
+        // scratch too): cfg8 2.09 ms with all sixteen, 1.79 with eight, 1.90 with four
         const long long nxt = grp + gridDim.x;
-        if (nxt < ngroups) load(nxt, 0, kPre);
+        load(nxt, 0, kPre, nxt < ngroups);
         fft1024_wave_lds(sbuf + w * kPassBuf, stw, L);
         __syncthreads();
-        if (nxt < ngroups) load(nxt, kPre, 16);
+        load(nxt, kPre, 16, nxt < ngroups);
         const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ob), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
