@@ -209,6 +209,16 @@ __device__ __forceinline__ void st_nt2(f2* p, f2 v) {
 // FP32 throughout (sdsp_pk.hpp: each complex add / multiply is one or two
 // v_pk_* instructions, the same per-component operation order as cmul / dft4 /
 // tw16 above); pdft16 leaves X[k] of its 16 points at v[kout(k)].
+// store false: the same sixteen store instructions go to an empty buffer descriptor (dropped), so
+// every wave of a round issues the same number of memory operations -- the waits the compiler
+// places for the next round's loads then let this round's stores stay in flight
+typedef unsigned chan_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void chan_dummy_stores(f2* yf) {
+    const auto rz = __builtin_amdgcn_make_buffer_rsrc((void*)yf, (short)0, 0, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)  // distinct offsets: identical stores would be merged into one
+        __builtin_amdgcn_raw_buffer_store_b64(chan_u2{0u, 0u}, rz, 0, 8 * k, 2);
+}
 __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw& tw, int L, f2* __restrict__ yf,
                                              bool store) {
     using pk::kout;
@@ -242,13 +252,12 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
     pk::pdft16<false>(v);
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) v[kout(k1)] = pk::pmul(v[kout(k1)], tw.p2[k1 * 4 + n0]);
-    if (!store) return;  // uniform over the wave
     // P3: per block of four k1 = 4 b + i, transpose lanes n0 (lane bits 4, 5) x
     // registers i, so lane (n0, k2) holds the four n0-inputs of k1 = 4 b + n0; an
     // in-register DFT4 then gives X[k2 + 16 (4 b + n0) + 256 k0] = X[L + 64 b + 256 k0]:
     // every store instruction writes 512 bytes in lane order (8-byte and paired
     // 16-byte stores measured the same on cfg5)
-    f2* yl = yf + L;
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)yf, (short)0, store ? kM * 8 : 0, 0x00020000);
 #pragma unroll
     for (int bk = 0; bk < 4; ++bk) {
         f2 r[4] = {v[kout(4 * bk)], v[kout(4 * bk + 1)], v[kout(4 * bk + 2)], v[kout(4 * bk + 3)]};
@@ -258,7 +267,8 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
         row_swap<32>(r[1], r[3]);
         pk::pdft4<false>(r[0], r[1], r[2], r[3]);
 #pragma unroll
-        for (int k0 = 0; k0 < 4; ++k0) st_nt2(yl + 64 * bk + 256 * k0, r[k0]);
+        for (int k0 = 0; k0 < 4; ++k0)  // nontemporal (aux 2)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(chan_u2, r[k0]), ry, (L + 64 * bk + 256 * k0) * 8, 0, 2);
     }
 }
 
@@ -280,13 +290,17 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
                 int C, int xcd) {
     constexpr int kThreads = T, kNB = kM / T, kFrames = R;
     static_assert(R <= T / 64, "one frame per wave at most");
+    // branch taps resident in LDS ([tap][branch], conflict-free) when they fit beside the frame
+    // buffers; otherwise re-read from L2 every round
+    constexpr bool kTapsLds = (size_t)R * kM * 8 + sizeof(ChanTw) + (size_t)K * kM * 4 <= 160 * 1024;
     // the PFB ring holds the last 8 inputs of a branch, slot = frame mod 8: rounds of fewer
     // than 8 frames run as 8 / R sub-rounds of one 8-frame step (compile-time slots)
     constexpr int kStep = R < 8 ? 8 : R;
     static_assert(kStep % 8 == 0 && kStep % R == 0, "ring slots are frame mod 8");
     __shared__ ChanTw stw;
     __shared__ f2 sbuf[kFrames * kM];
-    const int t = threadIdx.x, L = t & 63, w = t >> 6;
+    __shared__ float ctap[kTapsLds ? K * kM : 1];
+    const int t = threadIdx.x, L = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform
     // chunks of F frames, C in all (cps per stream), walked by G resident
     // workgroups.  xcd: workgroup b runs on XCD b mod 8 (dispatch order), so XCD x
     // takes the contiguous range [x Q, (x+1) Q) of chunks, Q = ceil(C / 8), and its
@@ -343,13 +357,23 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
         }
     };
     float c[kNB][K];
+    if constexpr (kTapsLds) {
+        for (int e = t; e < K * kM; e += kThreads) ctap[(e % K) * kM + e / K] = cb[e];  // cb[p K + i] -> [i][p]
+    }
     auto load_taps = [&]() {
-        const float* cbp = cb;
-        asm volatile("" : "+s"(cbp));
+        if constexpr (kTapsLds) {
 #pragma unroll
-        for (int j = 0; j < kNB; ++j)
+            for (int j = 0; j < kNB; ++j)
 #pragma unroll
-            for (int i = 0; i < K; ++i) c[j][i] = cbp[branch(j) * K + i];
+                for (int i = 0; i < K; ++i) c[j][i] = ctap[i * kM + branch(j)];
+        } else {
+            const float* cbp = cb;
+            asm volatile("" : "+s"(cbp));
+#pragma unroll
+            for (int j = 0; j < kNB; ++j)
+#pragma unroll
+                for (int i = 0; i < K; ++i) c[j][i] = cbp[branch(j) * K + i];
+        }
     };
 
     // input sample of branch p_j at frame f: x[f*M + M-1-p_j]; before the call: history
@@ -364,20 +388,54 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
     // a round's new samples: plain loads when those frames exist (uniform test; a
     // per-load branch would serialise the HBM round trips), else guarded
     f2 nx[kFrames][kNB];
+    // a round's frames f0 >= 0 read only the call's input: buffer loads bounded by the end of the
+    // chunk (and of the call), so loads past it return zeros without traffic and every round
+    // issues the same loads, with no branch (a branch around them makes the compiler wait for
+    // all outstanding memory operations, this round's stores included, at the merge)
     auto load_round = [&](long long f0) {
         if (lab & 2) {
 #pragma unroll
             for (int f = 0; f < kFrames; ++f)
 #pragma unroll
                 for (int j = 0; j < kNB; ++j) nx[f][j] = ring[j][(f + 3) & 7];
-        } else if (f0 + kFrames <= frames) {
-#pragma unroll
-            for (int f = 0; f < kFrames; ++f) load_pair(xs + (f0 + f) * kM, nx[f]);
         } else {
+            const long long q0 = f0 * kM, qe0 = m_end * kM, qe = qe0 < n ? qe0 : n, rem = qe - q0;
+            const unsigned nrec = rem <= 0 ? 0u : (unsigned)((rem < (long long)kFrames * kM ? rem : (long long)kFrames * kM) * 8);
+            const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(xs + (rem > 0 ? q0 : 0)), (short)0, nrec, 0x00020000);
 #pragma unroll
-            for (int f = 0; f < kFrames; ++f)
-#pragma unroll
-                for (int j = 0; j < kNB; ++j) nx[f][j] = ext(f0 + f, j);
+            for (int f = 0; f < kFrames; ++f) {
+                if constexpr (kPair) {
+                    const pk::f4v q = __builtin_bit_cast(pk::f4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                    rx, (unsigned)(f * kM + kM - 2 - 2 * t) * 8, 0, 0));
+                    nx[f][0] = f2{q.z, q.w};  // branch 2t:   x[M-1-2t]
+                    nx[f][1] = f2{q.x, q.y};  // branch 2t+1: x[M-2-2t]
+                } else if constexpr (kFrames != 8 || !PF) {
+                    nx[f][0] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                          rx, (unsigned)(f * kM + kM - 1 - t) * 8, 0, 0));
+                } else {
+                    // untracked by the compiler (its waits, merged over the loop's paths, would cover
+                    // this round's stores too): the wait is wait_round's, after those stores
+                    const unsigned long long a = (unsigned long long)(xs + (rem > 0 ? q0 : 0));
+                    typedef unsigned u4s __attribute__((ext_vector_type(4)));
+                    const u4s rw = {(unsigned)a, (unsigned)(a >> 32) & 0xffffu, nrec, 0x00020000u};
+                    f2 r;
+                    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen"
+                                 : "=v"(r)
+                                 : "v"((unsigned)(f * kM + kM - 1 - t) * 8), "s"(rw)
+                                 : "memory");
+                    nx[f][0] = r;
+                }
+            }
+        }
+    };
+    // the prefetched round has landed: every wave issued exactly sixteen stores after its loads
+    // (the frame's, or sixteen dropped ones), so vmcnt(16) waits for the loads alone
+    auto wait_round = [&](bool first) {
+        if constexpr (!kPair && kFrames == 8 && PF) {
+            if (first) asm volatile("s_waitcnt vmcnt(0)" : "+v"(nx[0][0]), "+v"(nx[1][0]), "+v"(nx[2][0]), "+v"(nx[3][0]),
+                                    "+v"(nx[4][0]), "+v"(nx[5][0]), "+v"(nx[6][0]), "+v"(nx[7][0]) :: "memory");
+            else asm volatile("s_waitcnt vmcnt(16)" : "+v"(nx[0][0]), "+v"(nx[1][0]), "+v"(nx[2][0]), "+v"(nx[3][0]),
+                              "+v"(nx[4][0]), "+v"(nx[5][0]), "+v"(nx[6][0]), "+v"(nx[7][0]) :: "memory");
         }
     };
     __syncthreads();
@@ -411,13 +469,16 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
         // PF: the next round's samples are requested before this round's FFT stores,
         // so waiting for them (vmcnt counts loads and stores in issue order) never
         // waits for the stores
-        if (PF) load_round(m0);
+        if (PF) {
+            load_round(m0);
+            wait_round(true);  // the chunk's first round: once per chunk
+        }
         for (long long mb = m0; mb < m_end; mb += kStep) {
             load_taps();
 #pragma unroll
             for (int sub = 0; sub < kStep / kFrames; ++sub) {
                 const long long mr = mb + (long long)sub * kFrames;
-                if (mr >= m_end) break;  // uniform
+                if (sub > 0 && mr >= m_end) break;  // uniform (sub 0 starts below m_end)
                 if (!PF) load_round(mr);
                 // PFB: frame mr + g into buffer g (ring slot (sub R + g) mod 8); per component
                 // acc = fma(c_i, h, acc), one v_pk_fma_f32 per tap
@@ -441,10 +502,11 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
                         for (int j = 0; j < kNB; ++j) sbuf[g * kM + t + kThreads * j] = pacc[j];
                     }
                 }
-                if (PF && mr + kFrames < m_end) load_round(mr + kFrames);
+                if (PF) load_round(mr + kFrames);  // past the chunk: zeros, no traffic
                 __syncthreads();
                 const long long f = mr + w;
                 if (w >= kFrames) {  // uniform per wave: no frame for this wave in the round
+                    chan_dummy_stores(ys);
                 } else if (lab & 1) {
                     if (!(lab & 4) && f < m_end)
 #pragma unroll
@@ -452,6 +514,7 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
                 } else {
                     fft1024_chan(sbuf + w * kM, stw, L, ys + f * kM, f < m_end && !(lab & 4));
                 }
+                if (PF) wait_round(false);
                 __syncthreads();
             }
         }
