@@ -635,7 +635,7 @@ class Cfg9AGC:
         self.samples_per_step = total
         self.bytes_per_step = 32 * total
         self.dtype = "c64 (f64 gain recurrence with exp/ln/log10 per sample)"
-        self.kernel = "agc_kernel<true> (one lane per channel, 8-sample LDS runs)"
+        self.kernel = "agc_pipe_kernel<true, 16> (one lane per channel, 16-sample LDS runs, next run prefetched)"
         self.parity_check = "max |y - ref| / max |ref| over the first 64 channels vs the f64 restatement (tolerance 1e-12)"
         self.workload = "cfg9: AGC(bw 0.02, squelch -30 dB) bank, 2^18 channels x 2^10 Complex<f64> samples"
         self.algo_name = "agc"

@@ -487,6 +487,115 @@ __global__ void __launch_bounds__(64, 4) agc_kernel(const AgcSample<CPLX>* __res
     if (me < channels) state[me] = s;
 }
 
+// agc_kernel with the next chunk's loads in flight across this chunk's gain chain: whole chunks
+// through buffer loads / stores bounded by the workgroup's channels (rows past the last channel
+// read zeros and drop their stores, so no branch sits around a memory op and the loads of chunk
+// i + 1, issued before the stores of chunk i, are waited for alone), the ragged last chunk as in
+// agc_kernel.  Offsets are 32-bit: n < 2^22 (the launcher routes larger n to agc_kernel).
+template <bool CPLX> struct AgcRaw;
+template <> struct AgcRaw<true> { typedef unsigned T __attribute__((ext_vector_type(4))); };
+template <> struct AgcRaw<false> { typedef unsigned T __attribute__((ext_vector_type(2))); };
+constexpr long long kAgcPipeMaxN = 1LL << 22;
+#ifndef SDSP_AGC_PIPE_S
+#define SDSP_AGC_PIPE_S 16
+#endif
+constexpr int kAgcPipeS = SDSP_AGC_PIPE_S;  // samples per channel per chunk
+
+template <bool CPLX, int S>
+__global__ void __launch_bounds__(64) agc_pipe_kernel(const AgcSample<CPLX>* __restrict__ x, AgcSample<CPLX>* __restrict__ y,
+                                                      long long n, sdsp_agc_state* __restrict__ state, long long channels) {
+    typedef typename AgcRaw<CPLX>::T V;
+    constexpr unsigned SZ = sizeof(AgcSample<CPLX>);
+    __shared__ AgcSample<CPLX> buf[64 * (S + 1)];
+    const int t = threadIdx.x;
+    const long long ch0 = (long long)blockIdx.x * 64;
+    const long long me = ch0 + t, nch = channels - ch0 < 64 ? channels - ch0 : 64;
+    sdsp_agc_state s;
+    double gthr = 0.0;
+    if (me < channels) {
+        s = state[me];
+        gthr = pow(10.0, -s.squelch_threshold / 20.0);
+    }
+    const long long nfull = n / S * S;
+    // lane e = t + 64 k of a row group: channel e / S, sample e % S of the chunk
+    unsigned off[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        const int e = t + 64 * k;
+        off[k] = (unsigned)(((long long)(e / S) * n + e % S) * SZ);
+    }
+    V r[S];
+    // chunk at i0 (whole chunks only; past nfull: an empty descriptor, no traffic)
+    auto rsrc = [&](const void* base, long long i0) {
+        const bool ok = i0 < nfull;
+        const unsigned nrec = ok ? (unsigned)((nch * n - i0) * SZ) : 0u;
+        return __builtin_amdgcn_make_buffer_rsrc((void*)((const AgcSample<CPLX>*)base + ch0 * n + (ok ? i0 : 0)), (short)0,
+                                                 nrec, 0x00020000);
+    };
+    auto load_chunk = [&](long long i0) {
+        const auto rx = rsrc(x, i0);
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            if constexpr (CPLX) r[k] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rx, off[k], 0, 0));
+            else r[k] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rx, off[k], 0, 0));
+        }
+    };
+    auto stage = [&] {  // the loaded chunk into the LDS rows
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int e = t + 64 * k;
+            buf[(e / S) * (S + 1) + e % S] = __builtin_bit_cast(AgcSample<CPLX>, r[k]);
+        }
+    };
+    load_chunk(0);
+    stage();
+    __syncthreads();
+    // rotated so that each wait for a chunk's loads sits in the same iteration as the loads,
+    // behind only that iteration's stores
+    for (long long i0 = 0; i0 < nfull; i0 += S) {
+        load_chunk(i0 + S);
+        if (me < channels)
+            for (int j = 0; j < S; ++j) {
+                AgcSample<CPLX>& v = buf[t * (S + 1) + j];
+                v = agc_execute<CPLX>(s, v, gthr);
+            }
+        __syncthreads();
+        const auto ry = rsrc(y, i0);
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int e = t + 64 * k;
+            const V v = __builtin_bit_cast(V, buf[(e / S) * (S + 1) + e % S]);
+            if constexpr (CPLX) __builtin_amdgcn_raw_buffer_store_b128(v, ry, off[k], 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b64(v, ry, off[k], 0, 0);
+        }
+        __syncthreads();
+        stage();
+        __syncthreads();
+    }
+    if (nfull < n) {  // the ragged last chunk
+        const long long i0 = nfull;
+        const int cnt = (int)(n - i0);
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int e = t + 64 * k, c = e / S, j = e % S;
+            if (j < cnt && ch0 + c < channels) buf[c * (S + 1) + j] = x[(ch0 + c) * n + i0 + j];
+        }
+        __syncthreads();
+        if (me < channels)
+            for (int j = 0; j < cnt; ++j) {
+                AgcSample<CPLX>& v = buf[t * (S + 1) + j];
+                v = agc_execute<CPLX>(s, v, gthr);
+            }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            const int e = t + 64 * k, c = e / S, j = e % S;
+            if (j < cnt && ch0 + c < channels) y[(ch0 + c) * n + i0 + j] = buf[c * (S + 1) + j];
+        }
+    }
+    if (me < channels) state[me] = s;
+}
+
 // init  :568-586 then set_signal_level  :416-428
 template <bool CPLX>
 __global__ void __launch_bounds__(64) agc_init_kernel(const AgcSample<CPLX>* __restrict__ x, long long n,
@@ -629,6 +738,16 @@ hipError_t launch_nco_mix(int prec, bool down, const void* x, void* y, size_t n,
 hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, size_t channels, hipStream_t s) {
     if (n == 0 || channels == 0) return hipSuccess;
     dim3 grid((unsigned)((channels + 63) / 64));
+    static const bool nopipe = std::getenv("SDSP_AGC_NOPIPE") != nullptr;  // A/B switch
+    if (!nopipe && (long long)n < kAgcPipeMaxN) {
+        if (cplx)
+            hipLaunchKernelGGL((agc_pipe_kernel<true, kAgcPipeS>), grid, dim3(64), 0, s, (const AgcSample<true>*)x,
+                               (AgcSample<true>*)y, (long long)n, (sdsp_agc_state*)state, (long long)channels);
+        else
+            hipLaunchKernelGGL((agc_pipe_kernel<false, kAgcPipeS>), grid, dim3(64), 0, s, (const AgcSample<false>*)x,
+                               (AgcSample<false>*)y, (long long)n, (sdsp_agc_state*)state, (long long)channels);
+        return hipGetLastError();
+    }
     if (cplx)
         hipLaunchKernelGGL(agc_kernel<true>, grid, dim3(64), 0, s, (const AgcSample<true>*)x, (AgcSample<true>*)y,
                            (long long)n, (sdsp_agc_state*)state, (long long)channels);

@@ -14,7 +14,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNEL = {2: ("fir_ols_os", "fft"), 3: ("sos_wscan", "scan"),
           4: ("decim_poly_kernel", "fma"), 5: ("chan1024_kernel", "chan"),
-          6: ("acorr_pipe_kernel", "acorr"), 7: ("nco_mix_kernel", "nco"), 8: ("fft1024_pipe", "fft"), 9: ("agc_kernel", "agc"),
+          6: ("acorr_pipe_kernel", "acorr"), 7: ("nco_mix_kernel", "nco"), 8: ("fft1024_pipe", "fft"), 9: ("agc_pipe_kernel", "agc"),
           10: ("interp_tile", "interp"), 11: ("sos_serial", "iir_serial_bank"), 12: ("sos_wscan", "normal_scan")}
 
 
