@@ -264,6 +264,29 @@ def test_agc_bank_and_device_lock():
     assert np.array_equal(g.get_gain(), gains)
 
 
+def test_agc_long_call_unpipelined_kernel():
+    """n >= 2^22 per channel runs agc_kernel (the pipelined kernel's buffer offsets are 32-bit):
+    both kernels against the restatement, two channels, n ragged against the chunk"""
+    import torch
+    import solid_dsp_amd as sd
+    rng = np.random.default_rng(23)
+    ch, n = 2, (1 << 22) + 5
+    x = ((rng.standard_normal((ch, n)) + 1j * rng.standard_normal((ch, n))) * 0.01).astype(C128)
+    g = sd.AGC(channels=ch)
+    g.set_bandwidth(0.02)
+    d_in = torch.from_numpy(x).to("cuda")
+    d_out = torch.empty_like(d_in)
+    g.execute_block_device(d_in, n, d_out, complex_=True, stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    y = d_out.cpu().numpy()
+    gains = g.get_gain()
+    for c in range(ch):
+        o = O.Agc()
+        o.set_bandwidth(0.02)
+        assert _close(y[c], o.execute_block(x[c])), c
+        assert abs(gains[c] - o.get_gain()) <= AGC_RTOL * o.get_gain()
+
+
 @pytest.mark.parametrize("thr", [-20.0, -20.0 - 1e-12, -20.0 + 1e-12, -19.99999, -20.00001])
 def test_agc_squelch_at_threshold(thr):
     """gain pinned exactly at the squelch threshold (x = 0.1, gain 10: E stays 1.0, the
