@@ -284,7 +284,7 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // = 5 / 6) halve / quarter the bytes a CU has in flight per round (R x 8 KB of loads and as
 // many of stores) and transform the round's frames on waves 0..R-1.
 template <int K, int T, bool PF, int R = T / 64>
-__global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD: 128 VGPRs
+__global__ void __launch_bounds__(T, T == 1024 ? 4 : 2)  // 1024 lanes: 4 waves per SIMD, 128 VGPRs
 chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
                 f2* __restrict__ y, const f2* __restrict__ tw, long long n, long long frames, int F, int cps,
                 int C, int xcd) {

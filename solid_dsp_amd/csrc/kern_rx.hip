@@ -226,9 +226,11 @@ __global__ void __launch_bounds__(kTile) acorr_pipe_kernel(const cpx<T>* __restr
     cpx<T> v[kLp];
     // interior tiles only (t_lo..t_hi): x[b0, b0 + ns) lies inside the call; the descriptor's
     // bound returns zeros past ns, so every lane issues the same kLp loads (no branches)
-    auto load = [&](long long tl) {
-        const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + tl * kOut - (K - 1) - d), (short)0, ns * kE,
-                                                          0x00020000);
+    // past the eighth's last tile (ok false): an empty descriptor, so the loads return zeros without
+    // touching memory and no branch sits around them
+    auto load = [&](long long tl, bool ok) {
+        const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + (ok ? tl : tile) * kOut - (K - 1) - d), (short)0,
+                                                          ok ? ns * kE : 0, 0x00020000);
 #pragma unroll
         for (int k = 0; k < kLp; ++k) {
             if constexpr (kE == 8)
@@ -237,17 +239,23 @@ __global__ void __launch_bounds__(kTile) acorr_pipe_kernel(const cpx<T>* __restr
                 v[k] = __builtin_bit_cast(cpx<T>, __builtin_amdgcn_raw_buffer_load_b128(rx, (t + k * kTile) * kE, 0, 0));
         }
     };
-    load(tile);
-    for (;;) {
-        const long long n0 = tile * kOut;
+    auto stage = [&] {
 #pragma unroll
         for (int k = 0; k < kLp; ++k) {
             const int i = t + k * kTile;
             if (i < ns) xs[i] = v[k];
         }
+    };
+    load(tile, true);
+    stage();
+    // rotated: each tile is staged at the end of the previous iteration, in the same iteration as
+    // its loads, so the compiler's wait for them sits behind only that iteration's stores (at the
+    // loop header it merged with the prologue's state and waited for the stores too)
+    for (;;) {
+        const long long n0 = tile * kOut;
         lds_sync();
         const long long nxt = tile + Gx;
-        if (nxt < e_hi) load(nxt);  // in flight across this tile's products, sums and stores
+        load(nxt, nxt < e_hi);  // in flight across this tile's products, sums and stores
 #pragma unroll
         for (int k = 0; k < (kOut + kPipeK - 1 + kTile - 1) / kTile; ++k) {
             const int s = t + k * kTile;
@@ -302,6 +310,7 @@ __global__ void __launch_bounds__(kTile) acorr_pipe_kernel(const cpx<T>* __restr
         if (nxt >= e_hi) break;
         tile = nxt;
         lds_sync();  // every read of xs and p done before the next tile is staged
+        stage();
     }
 }
 
