@@ -134,8 +134,64 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
         }
     };
     const bool fast = vec_ok;
-    if (fast && n >= T) load_tile(0);
-    for (long long k0 = 0; k0 < n; k0 += T) {
+    long long kstart = 0;
+    if (fast && (unsigned long long)n * 64ull * sizeof(I) < (1ull << 32)) {
+        // whole tiles, pipelined without branches around memory operations: buffer loads and stores
+        // bounded by the workgroup's channels (rows past nch read zeros and drop their stores), the
+        // loop rotated so each tile is staged in the iteration that loaded it -- the compiler's wait
+        // for the loads then sits behind only that iteration's stores
+        const long long nfull = n / T * T;
+        unsigned off[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int v = lane + 64 * j;
+            off[j] = (unsigned)(((long long)(v >> 4) * n + (long long)(v & 15) * E) * (long long)sizeof(I));
+        }
+        auto rsrc = [&](const void* base, long long k0) {
+            const bool ok = k0 < nfull;
+            const unsigned nrec = ok ? (unsigned)(((long long)nch * n - k0) * (long long)sizeof(I)) : 0u;
+            return __builtin_amdgcn_make_buffer_rsrc((void*)((const I*)base + c0 * n + (ok ? k0 : 0)), (short)0, nrec,
+                                                     0x00020000);
+        };
+        auto ld = [&](long long k0) {
+            const auto r = rsrc(x, k0);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) pre[j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off[j], 0, 0));
+        };
+        auto stage = [&] {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int v = lane + 64 * j;
+                *reinterpret_cast<v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16) = pre[j];
+            }
+        };
+        if (nfull > 0) {
+            ld(0);
+            stage();
+            for (long long k0 = 0; k0 < nfull; k0 += T) {
+                ld(k0 + T);  // past the last whole tile: an empty descriptor, no traffic
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
+                I* row = reinterpret_cast<I*>(lds + lane * kRow);
+                for (int e = 0; e < T; ++e) row[e] = sos_step<true, S>(coefs, row[e], w1, w2);
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
+                const auto r = rsrc(y, k0);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int v = lane + 64 * j;
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        *reinterpret_cast<const v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16), r, off[j], 0, 0);
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
+                stage();
+            }
+        }
+        kstart = nfull;  // the ragged tail (if any) below
+    }
+    if (fast && kstart == 0 && n >= T) load_tile(0);
+    for (long long k0 = kstart; k0 < n; k0 += T) {
         const bool full = fast && k0 + T <= n;
         if (full) {
 #pragma unroll
