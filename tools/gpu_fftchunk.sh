@@ -1,5 +1,6 @@
 #!/bin/bash
-# cfg8 sweep of the four-step FFT's batch chunking (SDSP_FFT_CHUNK transforms per pass pair)
+# cfg8 sweep of the four-step FFT's batch chunking (SDSP_FFT_CHUNK transforms per pass pair; the
+# runtime knob existed only for this experiment and was removed after it: logs in profiles/r03/lab/fft_chunk/)
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/fftchunk
 SDSP_FFT_CHUNK=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_fft.py -m gpu > gpurun_out/fftchunk/pytest_chunk1.log 2>&1 || { tail -5 gpurun_out/fftchunk/pytest_chunk1.log; exit 9; }
