@@ -151,7 +151,18 @@ typedef enum {
                                      handle's delay line (single-channel handles, not the FFT algorithm;
                                      reference arithmetic, bit-identical to the EXACT/FMA kernels);
                                      0 = every call launches device work (one-sample step kernel) */
-    SDSP_TUNE_HOST_BLOCK_MACS = 17 /* host-block threshold in multiply-adds (default 65536) */
+    SDSP_TUNE_HOST_BLOCK_MACS = 17, /* host-block threshold in multiply-adds (default 65536) */
+    SDSP_TUNE_FFT_GROUP = 18,      /* four-step passes on the generic pass kernel: at most this many
+                                      transforms per workgroup (1..64, default 4) */
+    SDSP_TUNE_FFT_WAVE1024 = 19,   /* four-step passes of 1024 points (c32): 16 (default) pipelined persistent
+                                      wave-FFT kernel, 1 / 8 one-shot with 16 / 8 transforms per workgroup,
+                                      0 the generic pass kernel */
+    SDSP_TUNE_ACORR_KERNEL = 20,   /* AutoCorrelator: 0 (default) pipelined kernel on interior tiles (delay
+                                      and window <= 128), one-shot kernel elsewhere; 1 the one-shot kernel
+                                      everywhere, delayed input staged in LDS (delay <= 256); 2 the one-shot
+                                      kernel with two loads per product */
+    SDSP_TUNE_AGC_KERNEL = 21      /* AGC bank: 0 (default) pipelined kernel for calls < 2^22 samples per
+                                      channel, 1 the plain per-sample kernel */
 } sdsp_tune_key;
 SDSP_API int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value);
 SDSP_API void sdsp_fir_destroy(sdsp_fir* h);        /* Drop */
@@ -305,6 +316,8 @@ SDSP_API void sdsp_fft_destroy(sdsp_fft* h);
 SDSP_API size_t sdsp_fft_len(const sdsp_fft* h);
 /* device plan: 0 direct DFT, 1 power of two in LDS, 2 Bluestein, 3 four-step power of two */
 SDSP_API int sdsp_fft_method(const sdsp_fft* h);
+/* kernel-variant knobs: SDSP_TUNE_FFT_GROUP, SDSP_TUNE_FFT_WAVE1024 (performance only) */
+SDSP_API int sdsp_fft_set_tuning(sdsp_fft* h, int key, int value);
 /* `batch` contiguous transforms of nfft complex samples */
 SDSP_API int sdsp_fft_execute(sdsp_fft* h, const void* in, void* out, size_t batch);
 SDSP_API int sdsp_fft_execute_device(sdsp_fft* h, const void* d_in, void* d_out, size_t batch, void* stream);
@@ -357,6 +370,8 @@ typedef struct sdsp_acorr sdsp_acorr;
 SDSP_API int sdsp_acorr_create(sdsp_acorr** out, size_t window_size, size_t delay, int precision, int device);
 SDSP_API void sdsp_acorr_destroy(sdsp_acorr* h);
 SDSP_API int sdsp_acorr_set_channels(sdsp_acorr* h, size_t channels);
+/* kernel-variant knob: SDSP_TUNE_ACORR_KERNEL (performance only) */
+SDSP_API int sdsp_acorr_set_tuning(sdsp_acorr* h, int key, int value);
 SDSP_API size_t sdsp_acorr_window_size(const sdsp_acorr* h);
 SDSP_API size_t sdsp_acorr_delay(const sdsp_acorr* h);
 /* reset  :76-85 */
@@ -436,6 +451,8 @@ typedef struct {  /* struct AGC  :96-108 */
 SDSP_API int sdsp_agc_create(sdsp_agc** out, size_t channels, int device);      /* AGC::new  :136-149 */
 SDSP_API void sdsp_agc_destroy(sdsp_agc* h);
 SDSP_API size_t sdsp_agc_channels(const sdsp_agc* h);
+/* kernel-variant knob: SDSP_TUNE_AGC_KERNEL (performance only) */
+SDSP_API int sdsp_agc_set_tuning(sdsp_agc* h, int key, int value);
 SDSP_API int sdsp_agc_reset(sdsp_agc* h);                                       /* :178-188 */
 /* execute_block  :273-285 (execute per sample :214-246); n samples per channel */
 SDSP_API int sdsp_agc_execute_block(sdsp_agc* h, int sample_type, const void* in, size_t n, void* out);

@@ -20,6 +20,7 @@ RR32, RC32, CC32, RR64, RC64, CC64 = range(6)
 ALGO_AUTO, ALGO_EXACT, ALGO_FMA, ALGO_FFT = range(4)
 # sdsp_tune_key values used by the bindings (include/sdsp.h)
 TUNE_HOST_STEP, TUNE_HOST_BLOCK_MACS = 16, 17
+TUNE_FFT_GROUP, TUNE_FFT_WAVE1024, TUNE_ACORR_KERNEL, TUNE_AGC_KERNEL = 18, 19, 20, 21
 
 _PAIRS = {
     (np.dtype(np.float32), np.dtype(np.float32)): RR32,
@@ -157,6 +158,9 @@ def _optional_sigs():
         "sdsp_iir_set_algo": (i, [vp, i]),
         "sdsp_iir_set_tuning": (i, [vp, i, i]),
         "sdsp_chan_set_tuning": (i, [vp, i, i]),
+        "sdsp_fft_set_tuning": (i, [vp, i, i]),
+        "sdsp_acorr_set_tuning": (i, [vp, i, i]),
+        "sdsp_agc_set_tuning": (i, [vp, i, i]),
         "sdsp_iir_output_count": (sz, [vp, sz]),
         "sdsp_iir_execute_block": (i, [vp, vp, sz, vp, szp]),
         "sdsp_iir_execute_block_device": (i, [vp, vp, sz, vp, szp, vp]),

@@ -63,6 +63,10 @@ class AGC:
             L.lib().sdsp_agc_destroy(h)
             self._h = None
 
+    def set_tuning(self, key: int, value: int):
+        """Kernel-variant knob (L.TUNE_AGC_KERNEL; performance only, same results)."""
+        _check(L.lib().sdsp_agc_set_tuning(self._h, int(key), int(value)))
+
     # ---- state ---------------------------------------------------------------
     def state(self, channel: int = 0) -> L.AgcState:
         st = L.AgcState()

@@ -194,15 +194,10 @@ template <int S> __device__ __forceinline__ void row_swap(f2& a, f2& b) {
     b = f2{bx, by};
 }
 
-#ifdef SDSP_CHAN_LAB
-__device__ int g_chan_plain_st;  // lab: plain instead of nontemporal output stores
-__device__ int g_chan_nt_ld;     // lab: nontemporal input loads
-#endif
-__device__ __forceinline__ void st_nt2(f2* p, f2 v) {
-#ifdef SDSP_CHAN_LAB
-    if (g_chan_plain_st) { *p = v; return; }
-#endif
-    __builtin_nontemporal_store(v, p);
+// PLAIN: plain instead of nontemporal stores (a lab variant, LAB bit 32 below)
+template <bool PLAIN> __device__ __forceinline__ void st_nt2(f2* p, f2 v) {
+    if constexpr (PLAIN) *p = v;
+    else __builtin_nontemporal_store(v, p);
 }
 
 // one frame by one wave: buf holds v[p] at p; natural-order X to yf.  Packed
@@ -283,7 +278,10 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // R (frames per round) defaults to one per wave; R = 8 / 4 with T = 1024 (SDSP_TUNE_CHAN_STREAMING
 // = 5 / 6) halve / quarter the bytes a CU has in flight per round (R x 8 KB of loads and as
 // many of stores) and transform the round's frames on waves 0..R-1.
-template <int K, int T, bool PF, int R = T / 64>
+// LAB selects compile-time variants for in-process A/B runs (tools/lab/chan_lab.hip; the
+// product kernels are LAB = 0): 1 no FFT, 2 no loads, 4 no stores (ablations); 8 / 16 odd
+// workgroups start ~6.8 / ~3.4 us late; 32 plain stores; 64 nontemporal loads.
+template <int K, int T, bool PF, int R = T / 64, int LAB = 0>
 __global__ void __launch_bounds__(T, T == 1024 ? 4 : 2)  // 1024 lanes: 4 waves per SIMD, 128 VGPRs
 chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
                 f2* __restrict__ y, const f2* __restrict__ tw, long long n, long long frames, int F, int cps,
@@ -309,16 +307,13 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
     // frames were just read by the workgroup on the chunk before (same L2).
     // Without xcd: chunk b + k G.
     const unsigned G = gridDim.x, bid = blockIdx.x;
-#ifdef SDSP_CHAN_LAB
-    const int lab = xcd >> 4;  // ablations (tools/chan_ab.py): 1 no FFT, 2 no loads, 4 no stores
-    xcd &= 1;
-    if ((lab & 24) && ((bid >> 3) & 1)) {  // stagger: desynchronise the rounds of neighbouring workgroups
-        const int ns = ((lab & 8) ? 2 : 0) + ((lab & 16) ? 1 : 0);
-        for (int i = 0; i < ns; ++i) __builtin_amdgcn_s_sleep(127);
+    constexpr int lab = LAB & 7;
+    if constexpr ((LAB & 24) != 0) {
+        if ((bid >> 3) & 1) {  // stagger: desynchronise the rounds of neighbouring workgroups
+            constexpr int ns = ((LAB & 8) ? 2 : 0) + ((LAB & 16) ? 1 : 0);
+            for (int i = 0; i < ns; ++i) __builtin_amdgcn_s_sleep(127);
+        }
     }
-#else
-    constexpr int lab = 0;
-#endif
     const unsigned Q = xcd ? (C + 7) / 8 : C, Gx = xcd ? G / 8 : G;
     const unsigned c_lo = xcd ? (bid & 7) * Q : 0, c_hi = c_lo + Q < (unsigned)C ? c_lo + Q : C;
     const unsigned c_first = c_lo + (xcd ? bid >> 3 : bid);
@@ -341,19 +336,14 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
     auto load_pair = [&](const f2* xf, f2 (&v)[kNB]) {
         if constexpr (kPair) {
             const pk::f4v* qp = reinterpret_cast<const pk::f4v*>(xf + kM - 2 - 2 * t);
-#ifdef SDSP_CHAN_LAB
-            const pk::f4v q = g_chan_nt_ld ? __builtin_nontemporal_load(qp) : *qp;
-#else
-            const pk::f4v q = *qp;
-#endif
+            pk::f4v q;
+            if constexpr ((LAB & 64) != 0) q = __builtin_nontemporal_load(qp);
+            else q = *qp;
             v[0] = f2{q.z, q.w};  // branch 2t:   x[M-1-2t]
             v[1] = f2{q.x, q.y};  // branch 2t+1: x[M-2-2t]
         } else {
-#ifdef SDSP_CHAN_LAB
-            v[0] = g_chan_nt_ld ? __builtin_nontemporal_load(xf + kM - 1 - t) : xf[kM - 1 - t];
-#else
-            v[0] = xf[kM - 1 - t];
-#endif
+            if constexpr ((LAB & 64) != 0) v[0] = __builtin_nontemporal_load(xf + kM - 1 - t);
+            else v[0] = xf[kM - 1 - t];
         }
     };
     float c[kNB][K];
@@ -510,7 +500,7 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
                 } else if (lab & 1) {
                     if (!(lab & 4) && f < m_end)
 #pragma unroll
-                        for (int k = 0; k < 16; ++k) st_nt2(ys + f * kM + L + 64 * k, sbuf[w * kM + L + 64 * k]);
+                        for (int k = 0; k < 16; ++k) st_nt2<(LAB & 32) != 0>(ys + f * kM + L + 64 * k, sbuf[w * kM + L + 64 * k]);
                 } else {
                     fft1024_chan(sbuf + w * kM, stw, L, ys + f * kM, f < m_end && !(lab & 4));
                 }
@@ -706,18 +696,10 @@ fft1024_pipe_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 
 }  // namespace
 
-#ifdef SDSP_CHAN_LAB
-static int g_chan_lab = 0;
-extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) {
-    g_chan_lab = (v & 7) | ((v >> 2) & 24);  // bits 32 / 64: odd workgroups start ~6.8 / ~3.4 us late
-    const int plain = (v >> 3) & 1, ntld = (v >> 4) & 1;  // bit 8: plain stores, bit 16: nontemporal loads
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chan_plain_st), &plain, sizeof(int));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chan_nt_ld), &ntld, sizeof(int));
-}
-#endif
-
-// M = 1024, complex f32, K <= 8 taps per branch; false = not applicable
-bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
+// M = 1024, complex f32, K <= 8 taps per branch; false = not applicable.  LAB: chan1024_kernel
+// (0 = the product kernels)
+template <int LAB>
+bool try_launch_chan1024_t(const ChanArgs& a, hipStream_t s, hipError_t* err) {
     if (a.M != 1024 || a.K < 1 || a.K > 8 || a.fast <= 0) return false;
     // the 512-thread form loads 16 bytes per lane: 1024-thread form for an input
     // that is only 8-byte aligned
@@ -739,21 +721,18 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
         if (G == 0) xcd = 0, G = C;
     }
     dim3 grid((unsigned)G);
-#ifdef SDSP_CHAN_LAB
-    xcd |= g_chan_lab << 4;
-#endif
-#define SDSP_CHAN_T(KV, T, PF, ...)                                                                        \
-    hipLaunchKernelGGL((chan1024_kernel<KV, T, PF, ##__VA_ARGS__>), grid, dim3(T), 0, s, (const f2*)a.x, (const f2*)a.hist,     \
+#define SDSP_CHAN_T(KV, T, PF, R)                                                                          \
+    hipLaunchKernelGGL((chan1024_kernel<KV, T, PF, R, LAB>), grid, dim3(T), 0, s, (const f2*)a.x, (const f2*)a.hist, \
                        (const float*)a.cb, (f2*)a.y, (const f2*)a.tw, (long long)a.n, (long long)a.frames, F, (int)cps, \
                        (int)C, xcd)
-#define SDSP_CHAN(KV)                                                                      \
-    case KV:                                                                               \
-        if (var == 2) SDSP_CHAN_T(KV, 512, false);                                         \
-        else if (var == 3) SDSP_CHAN_T(KV, 1024, true);                                    \
-        else if (var == 4) SDSP_CHAN_T(KV, 512, true);                                     \
-        else if (var == 5) SDSP_CHAN_T(KV, 1024, true, 8);                                 \
-        else if (var == 6) SDSP_CHAN_T(KV, 1024, true, 4);                                 \
-        else SDSP_CHAN_T(KV, 1024, false);                 \
+#define SDSP_CHAN(KV)                                                   \
+    case KV:                                                            \
+        if (var == 2) SDSP_CHAN_T(KV, 512, false, 8);                   \
+        else if (var == 3) SDSP_CHAN_T(KV, 1024, true, 16);             \
+        else if (var == 4) SDSP_CHAN_T(KV, 512, true, 8);               \
+        else if (var == 5) SDSP_CHAN_T(KV, 1024, true, 8);              \
+        else if (var == 6) SDSP_CHAN_T(KV, 1024, true, 4);              \
+        else SDSP_CHAN_T(KV, 1024, false, 16);                          \
         break;
     switch (a.K) {
         SDSP_CHAN(1) SDSP_CHAN(2) SDSP_CHAN(3) SDSP_CHAN(4) SDSP_CHAN(5) SDSP_CHAN(6) SDSP_CHAN(7) SDSP_CHAN(8)
@@ -764,20 +743,20 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
     return true;
 }
 
+bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
+    return try_launch_chan1024_t<0>(a, s, err);
+}
+
 // four-step pass of L = 1024 on the wave FFT; false = not applicable
 bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
-    // SDSP_FFT_WAVE1024: 16 (default) the pipelined persistent kernel, 1 the one-shot kernel
-    // with 16 transforms per workgroup, 8 one-shot with 8, 0 the generic Stockham pass
-    static const int tpb = [] {
-        const char* e = std::getenv("SDSP_FFT_WAVE1024");
-        const int v = e ? std::atoi(e) : 16;
-        return v == 0 || v == 8 || v == 1 ? v : 16;
-    }();
+    // p.wave1024 (SDSP_TUNE_FFT_WAVE1024): 16 (default) the pipelined persistent kernel, 1 the
+    // one-shot kernel with 16 transforms per workgroup, 8 one-shot with 8, 0 the generic Stockham pass
+    const int tpb = p.wave1024 == 0 || p.wave1024 == 8 || p.wave1024 == 1 ? p.wave1024 : 16;
     if (tpb == 0 || p.L != 1024 || p.count % 16 != 0 || p.G % 16 != 0) return false;
     if (!(p.S1 == 1 || p.Si == 1) || !(p.T1 == 1 || p.So == 1)) return false;
     if (p.Ntw && (p.Ntw != (1LL << 20) || !p.twx)) return false;
     if (tpb == 16) {
-        int dev = 0, cus = 256;
+        int dev = 0, cus = 256;  // (the current device's CU count)
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const long long groups = p.count / 16;
         const dim3 g2((unsigned)(groups < cus ? groups : cus));

@@ -239,11 +239,7 @@ hipError_t launch_fft_pass_t(const FftPass& p, hipStream_t s) {
     const int L = p.L;
     // transforms per workgroup: up to kMaxGroup interleaved transforms in <= kLdsCap
     // bytes of LDS (two L-point buffers each), dividing G; <= 1024 threads
-    static const int kMaxGroup = [] {
-        const char* e = std::getenv("SDSP_FFT_GROUP");
-        const int v = e ? std::atoi(e) : 4;
-        return v >= 1 && v <= 64 ? v : 4;
-    }();
+    const int kMaxGroup = p.group >= 1 && p.group <= 64 ? p.group : 4;
     constexpr size_t kLdsCap = 128 * 1024;
     const size_t per = 2 * (size_t)L * sizeof(c2<T>);
     int tpb = 1;

@@ -39,12 +39,6 @@ namespace {
 
 constexpr int kWsThreads = 256;
 
-#ifdef SDSP_IIR_LAB
-// ablations for tools/iir_ab.py (lab builds only, never in libsdsp.so): 1 no zero-state
-// run, 2 no scan, 4 no correction, 8 no HBM loads, 16 no HBM stores; variants:
-// 32 plain (not nontemporal) loads, 64 plain stores
-__device__ int g_iir_lab;
-#endif
 constexpr int kWsWaves = kWsThreads / 64;
 
 // chunk of CB bytes per lane (B = CB / sizeof(I) samples); LDS rows padded by
@@ -165,7 +159,10 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // FORM: 0 correction by the state response, next tile prefetched into registers; 1 a
 // rerun from the true state instead of the correction; 2 the correction without the
 // register prefetch (fewer registers: more waves per SIMD hide the tile loads instead)
-template <int S, int ND, typename C, typename I, int CB, int FORM>
+// LAB selects compile-time variants for in-process A/B runs (tools/lab/iir_lab.hip; the product
+// kernels are LAB = 0): ablations 1 no zero-state run, 2 no scan, 4 no correction, 8 no HBM
+// loads, 16 no HBM stores; variants 32 plain (not nontemporal) loads, 64 plain stores
+template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
@@ -199,11 +196,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         return k % Mi == 0 ? x[k / Mi] : zero_v<I>();
     };
 
-#ifdef SDSP_IIR_LAB
-    const int lab = __builtin_amdgcn_readfirstlane(g_iir_lab);
-#else
-    constexpr int lab = 0;
-#endif
+    constexpr int lab = LAB;
     // XCD-ordered blocks (gridDim.x is a multiple of 8): block b runs on XCD b % 8 and
     // takes the (b / 8)-th block of that XCD's contiguous eighth, so each XCD streams
     // one window of neighbouring segments (cfg3: -1.6 %, the HBM-only pattern -2 %)
@@ -796,26 +789,22 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-#ifdef SDSP_IIR_LAB
-static int g_iir_lab_host = 0;
-#endif
-
 template <int CB> int wscan_tpw(long long nch) {
     // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
     int tpw = (int)(nch / (64LL * 4096));
     return tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
 }
 
-template <typename C, typename I, int S, int CB, int FORM, int ND = 0>
-hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
+// LAB: sos_wscan_kernel (0 = the product kernel); tpw_force > 0 sets the tiles per wave of a
+// warm-up scan (lab runs)
+template <typename C, typename I, int S, int CB, int FORM, int ND = 0, int LAB = 0>
+hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st, int tpw_force = 0) {
     constexpr int B = ws_chunk<I, CB>::B;
     constexpr int D = ND ? ND : 2 * S;
     const long long nd = (long long)a.n * a.Mi;  // domain samples
     const long long nch = (nd + B - 1) / B;
     int tpw = wscan_tpw<CB>(nch);
-#ifdef SDSP_IIR_LAB
-    if (a.wc > 0 && ((g_iir_lab_host >> 8) & 15)) tpw = (g_iir_lab_host >> 8) & 15;  // lab: tiles per wave
-#endif
+    if (a.wc > 0 && tpw_force > 0) tpw = tpw_force;
     const long long segc = (long long)tpw * 64 - a.wc;
     const long long waves = (nch + segc - 1) / segc;
     const bool exact = a.wc == 0;  // exact inter-wave carries: aggregate pass + carry scan first
@@ -829,14 +818,14 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st) {
     const long long j0 = a.Md > 1 ? (long long)((a.Md - 1 - a.phase) % a.Md) : 0;  // first emitting domain index
     const long long ny = a.Md > 1 ? (long long)a.nout : nd;
     if (exact) {
-        hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
+        hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
                            (I*)a.y, (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out,
                            nd, 0, tpw, vec_ok, a.Mi, a.Md, j0, ny, (const I*)nullptr, (I*)a.G, waves);
         hipLaunchKernelGGL((wscan_carry_kernel<D, C, I>), dim3((unsigned)a.channels), dim3(256), 0, st,
                            (const I*)a.G, (I*)a.Cin, (const C*)a.Phi + (size_t)(tpw - 1) * D * D, (const I*)a.st_in,
                            waves);
     }
-    hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
+    hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
                        tpw, vec_ok, a.Mi, a.Md, j0, ny, exact ? (const I*)a.Cin : (const I*)nullptr, (I*)nullptr,
                        waves);
@@ -892,12 +881,6 @@ hipError_t launch_wscan_dt(const IirArgs& a, hipStream_t st) {
 
 }  // namespace
 
-#ifdef SDSP_IIR_LAB
-extern "C" __attribute__((visibility("default"))) int sdsp_lab_set_iir_ablation(int v) {
-    g_iir_lab_host = v;  // bits 8-11: tiles per wave (warm-up scans)
-    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_iir_lab), &v, sizeof(int));
-}
-#endif
 
 size_t iir_wscan_waves(int dtype, const IirArgs& a, int* tpw_out) {
     const bool c128 = a.ws_variant == 1 || a.ws_variant == 5;

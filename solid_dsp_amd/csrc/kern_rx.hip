@@ -31,7 +31,9 @@
 // stages kAgcS samples of each through LDS so that HBM sees 16 * kAgcS-byte
 // runs per channel instead of one sample per lane per row.
 #include "sdsp.h"
-#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 
@@ -630,28 +632,44 @@ static size_t acorr_lds_bytes(size_t elem, int d, int K, bool stage) {
     return (np + nx) * elem;
 }
 
+// resident one-wave workgroups of acorr_pipe_kernel on the current device (CU count x occupancy
+// at `lds` bytes), looked up once per (device, precision, LDS size)
+static long long acorr_pipe_slots(int prec, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, size_t>, long long> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const auto key = std::make_tuple(dev, prec, lds);
+    std::lock_guard<std::mutex> g(mu);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 256, per_cu = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (prec == 0)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, acorr_pipe_kernel<float>, kTile, lds);
+    else
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, acorr_pipe_kernel<double>, kTile, lds);
+    const long long res = (long long)(per_cu > 0 ? per_cu : 8) * cus;
+    cache.emplace(key, res);
+    return res;
+}
+
 hipError_t launch_acorr(int prec, const void* x, const void* hist, void* y, size_t n, int H, int d, int K,
-                        size_t channels, hipStream_t s) {
+                        size_t channels, hipStream_t s, int kernel) {
     if (n == 0) return hipSuccess;
     dim3 grid((unsigned)((n + kOut - 1) / kOut), (unsigned)channels);
-    static const bool nostage = std::getenv("SDSP_ACORR_NOSTAGE") != nullptr;  // A/B switch
-    static const bool pipe = std::getenv("SDSP_ACORR_NOPIPE") == nullptr;      // A/B switch
+    const bool nostage = kernel == 2, pipe = kernel == 0;
     if (pipe && K >= 1 && K <= kPipeK && d <= kPipeD) {
         // interior tiles (whole input window and all outputs inside the call) on the pipelined
         // kernel; the edge tiles on the one-shot kernel
         const long long ntiles = (long long)((n + kOut - 1) / kOut);
         const long long t_lo = (K - 1 + d + kOut - 1) / kOut, t_hi = (long long)(n / kOut);
         if (t_hi > t_lo) {
-            int cus = 256, per_cu = 0;
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
             const size_t elem = prec == 0 ? sizeof(c32) : sizeof(c64);
             const size_t lds2 = ((size_t)pad8(kOut + K - 1) + 1 + (size_t)(kOut + K - 1 + d)) * elem;
-            // one persistent wave per resident slot (registers / LDS decide how many per CU)
-            if (prec == 0)
-                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, acorr_pipe_kernel<float>, kTile, lds2);
-            else
-                (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, acorr_pipe_kernel<double>, kTile, lds2);
-            const long long res = (long long)(per_cu > 0 ? per_cu : 8) * cus;
+            // one persistent wave per resident slot (registers / LDS decide how many per CU): the
+            // current device's CU count and the kernel's occupancy at this LDS size, cached
+            const long long res = acorr_pipe_slots(prec, lds2);
             const long long nt = t_hi - t_lo;
             long long G = nt < res ? nt : res;
             G = (G + 7) / 8 * 8;  // whole workgroups per XCD (surplus ones find no tile and return)
@@ -744,11 +762,11 @@ hipError_t launch_nco_mix(int prec, bool down, const void* x, void* y, size_t n,
     return hipGetLastError();
 }
 
-hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, size_t channels, hipStream_t s) {
+hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, size_t channels, hipStream_t s,
+                      bool pipe) {
     if (n == 0 || channels == 0) return hipSuccess;
     dim3 grid((unsigned)((channels + 63) / 64));
-    static const bool nopipe = std::getenv("SDSP_AGC_NOPIPE") != nullptr;  // A/B switch
-    if (!nopipe && (long long)n < kAgcPipeMaxN) {
+    if (pipe && (long long)n < kAgcPipeMaxN) {
         if (cplx)
             hipLaunchKernelGGL((agc_pipe_kernel<true, kAgcPipeS>), grid, dim3(64), 0, s, (const AgcSample<true>*)x,
                                (AgcSample<true>*)y, (long long)n, (sdsp_agc_state*)state, (long long)channels);

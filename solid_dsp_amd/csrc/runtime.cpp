@@ -693,7 +693,7 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
     SDSP_TRY(launch_hist_update(h->dtype, d_in, hist, h->d_hist[h->cur ^ 1].p, n, (int)h->L - 1, h->channels, s),
              "history update");
     h->cur ^= 1;
-    if (s != h->stream) SDSP_TRY(h->fence.record(s), "record fence");
+    SDSP_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 
@@ -1023,6 +1023,8 @@ int sdsp_pfb_execute_block_device(sdsp_pfb* h, const void* d_in, size_t n, void*
         set_error("input and output blocks overlap (in-place filtering is not supported)");
         return SDSP_E_INVALID_ARGUMENT;
     }
+    // work queued on another stream (the fence) reads or writes the window this launch uses
+    SDSP_TRY(h->fence.order_before(s), "order after queued work");
     PfbArgs a{d_in, h->d_hist[h->cur].p, h->d_cb.p, d_out, n, h->channels, (int)h->K, (int)h->M, (int)h->K,
               h->algo != SDSP_ALGO_FMA};
     SDSP_TRY(launch_pfb(h->dtype, a, s), "pfb");
@@ -1030,7 +1032,7 @@ int sdsp_pfb_execute_block_device(sdsp_pfb* h, const void* d_in, size_t n, void*
                                 h->channels, s),
              "window update");
     h->cur ^= 1;
-    if (s != h->stream) SDSP_TRY(h->fence.record(s), "record fence");
+    SDSP_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 

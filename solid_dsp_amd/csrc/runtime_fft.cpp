@@ -84,6 +84,7 @@ namespace {
 // decomposition N = N1 N2 (two strided passes, inter-pass twiddle) above
 struct Pow2Plan {
     size_t N = 0;
+    int group = 4, wave1024 = 16;  // pass kernel knobs (SDSP_TUNE_FFT_GROUP / SDSP_TUNE_FFT_WAVE1024)
     int logN = 0, l1 = 0, l2 = 0;
     DevBuf tw, tw1, tw2, twx;
     bool four_step() const { return N > 4096; }
@@ -119,11 +120,13 @@ struct Pow2Plan {
         }
         const long long n = (long long)N, N1 = 1LL << l1, N2 = 1LL << l2;
         // pass 1: columns n2 (length N1, stride N2) -> tmp[k1][n2] * W_N^(n2 k1)
-        FftPass p1{in, tmp, tw1.p, (int)N1, l1, (long long)batch * N2, N2, n, 1, N2, 1, N2, n, inverse, twx.p};
+        FftPass p1{in, tmp, tw1.p, (int)N1, l1, (long long)batch * N2, N2, n, 1, N2, 1, N2, n, inverse, twx.p,
+                   group, wave1024};
         hipError_t e = launch_fft_pass(f64, p1, s);
         if (e != hipSuccess) return e;
         // pass 2: rows k1 (length N2) -> out[k1 + N1 k2]
-        FftPass p2{tmp, out, tw2.p, (int)N2, l2, (long long)batch * N1, N1, n, N2, 1, 1, N1, 0, inverse};
+        FftPass p2{tmp, out, tw2.p, (int)N2, l2, (long long)batch * N1, N1, n, N2, 1, 1, N1, 0, inverse, nullptr,
+                   group, wave1024};
         return launch_fft_pass(f64, p2, s);
     }
 };
@@ -279,6 +282,15 @@ void sdsp_fft_destroy(sdsp_fft* h) {
 
 size_t sdsp_fft_len(const sdsp_fft* h) { return h ? h->N : 0; }
 
+int sdsp_fft_set_tuning(sdsp_fft* h, int key, int value) {
+    if (!h) return SDSP_E_INVALID_ARGUMENT;
+    if (key == SDSP_TUNE_FFT_GROUP && value >= 1 && value <= 64) h->p2.group = value;
+    else if (key == SDSP_TUNE_FFT_WAVE1024 && (value == 0 || value == 1 || value == 8 || value == 16))
+        h->p2.wave1024 = value;
+    else return SDSP_E_INVALID_ARGUMENT;
+    return SDSP_OK;
+}
+
 int sdsp_fft_execute_device(sdsp_fft* h, const void* d_in, void* d_out, size_t batch, void* stream) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (batch == 0) return SDSP_OK;
@@ -430,6 +442,7 @@ int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, voi
     }
     Guard g(h->device);
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    F_TRY(h->fence.order_before(s), "order after queued work");  // the history this launch reads
     ChanArgs a{d_in, h->hist[h->cur].p, h->cb.p, d_out, h->tw.p, (int)h->M, ilog2(h->M), (int)h->K, n, fr, h->streams};
     a.fast = h->fast;
     a.frames_per_block = h->fpb;
@@ -439,7 +452,7 @@ int sdsp_chan_execute_block_device(sdsp_chan* h, const void* d_in, size_t n, voi
     F_TRY(launch_hist_update(h->dtype, d_in, h->hist[h->cur].p, h->hist[h->cur ^ 1].p, n, H, h->streams, s),
           "history update");
     h->cur ^= 1;
-    if (s != h->stream) F_TRY(h->fence.record(s), "record fence");
+    F_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 

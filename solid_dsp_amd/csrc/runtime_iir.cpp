@@ -643,6 +643,8 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
         set_error("input and output blocks overlap (in-place filtering is not supported)");
         return SDSP_E_INVALID_ARGUMENT;
     }
+    // work queued on another stream (the fence) reads or writes the state this launch uses
+    IIR_TRY(h->fence.order_before(s), "order after queued work");
     const int Mi = h->mode == 2 ? (int)h->M : 1;
     const int Md = h->mode == 1 ? (int)h->M : 1;
     const size_t nd = n * Mi;
@@ -736,7 +738,7 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
     }
     h->cur ^= 1;
     if (h->mode == 1) h->phase = (h->phase + nd) % h->M;
-    if (s != h->stream) IIR_TRY(h->fence.record(s), "record fence");
+    IIR_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 

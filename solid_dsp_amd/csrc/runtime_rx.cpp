@@ -77,12 +77,15 @@ struct sdsp_acorr {
     DevBuf energy;   // [channels] f64
     DevBuf stage_in, stage_out;
     hipStream_t stream = nullptr;
+    int kernel = 0;  // SDSP_TUNE_ACORR_KERNEL
+    StreamFence fence;  // the last block queued (on a caller stream or the handle's)
     int K() const { return W > d ? (int)(W - d) : 0; }
 };
 
 namespace {
 int acorr_alloc(sdsp_acorr* h) {
     const size_t hb = h->channels * h->W * cbytes(h->prec);
+    R_TRY(h->fence.wait(), "wait for queued work");  // a queued block may still read the history
     for (int i = 0; i < 2; ++i) {
         R_TRY(h->hist[i].ensure(hb), "alloc history");
         R_TRY(hipMemsetAsync(h->hist[i].p, 0, hb, h->stream), "zero history");
@@ -134,6 +137,7 @@ void sdsp_acorr_destroy(sdsp_acorr* h) {
     if (!h) return;
     {
         Guard g(h->device);
+        (void)h->fence.wait();
         if (h->stream) {
             (void)hipStreamSynchronize(h->stream);
             (void)hipStreamDestroy(h->stream);
@@ -145,6 +149,12 @@ void sdsp_acorr_destroy(sdsp_acorr* h) {
         h->stage_out.release();
     }
     delete h;
+}
+
+int sdsp_acorr_set_tuning(sdsp_acorr* h, int key, int value) {
+    if (!h || key != SDSP_TUNE_ACORR_KERNEL || value < 0 || value > 2) return SDSP_E_INVALID_ARGUMENT;
+    h->kernel = value;
+    return SDSP_OK;
 }
 
 int sdsp_acorr_set_channels(sdsp_acorr* h, size_t channels) {
@@ -166,14 +176,18 @@ size_t sdsp_acorr_delay(const sdsp_acorr* h) { return h ? h->d : 0; }
 // push n samples per channel; with d_out, the execute() value after every push
 static int acorr_run(sdsp_acorr* h, const void* d_in, size_t n, void* d_out, hipStream_t s) {
     if (n == 0) return SDSP_OK;
+    // blocks queued on another stream read and write the history this launch uses
+    R_TRY(h->fence.order_before(s), "order after queued work");
     const void* hist = h->hist[h->cur].p;
     if (d_out)
-        R_TRY(launch_acorr(h->prec, d_in, hist, d_out, n, (int)h->W, (int)h->d, h->K(), h->channels, s), "acorr");
+        R_TRY(launch_acorr(h->prec, d_in, hist, d_out, n, (int)h->W, (int)h->d, h->K(), h->channels, s, h->kernel),
+              "acorr");
     R_TRY(launch_acorr_energy(h->prec, d_in, hist, n, (int)h->W, (int)h->W, h->channels, (double*)h->energy.p, s),
           "acorr energy");
     R_TRY(launch_hist_update(hist_dtype(h->prec), d_in, hist, h->hist[h->cur ^ 1].p, n, (int)h->W, h->channels, s),
           "history update");
     h->cur ^= 1;
+    R_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;
 }
 
@@ -221,6 +235,7 @@ int sdsp_acorr_execute(sdsp_acorr* h, void* out) {
     Guard g(h->device);
     const size_t bytes = h->channels * cbytes(h->prec);
     R_TRY(h->stage_out.ensure(bytes), "stage out");
+    R_TRY(h->fence.order_before(h->stream), "order after queued work");
     R_TRY(launch_acorr_current(h->prec, h->hist[h->cur].p, h->stage_out.p, (int)h->W, (int)h->d, h->K(), h->channels,
                                h->stream),
           "acorr execute");
@@ -232,6 +247,7 @@ int sdsp_acorr_execute(sdsp_acorr* h, void* out) {
 int sdsp_acorr_get_energy(sdsp_acorr* h, double* energy) {
     if (!h || !energy) return SDSP_E_INVALID_ARGUMENT;
     Guard g(h->device);
+    R_TRY(h->fence.order_before(h->stream), "order after queued work");
     R_TRY(hipMemcpyAsync(energy, h->energy.p, h->channels * 8, hipMemcpyDeviceToHost, h->stream), "D2H");
     R_TRY(hipStreamSynchronize(h->stream), "sync");
     return SDSP_OK;
@@ -240,6 +256,7 @@ int sdsp_acorr_get_energy(sdsp_acorr* h, double* energy) {
 int sdsp_acorr_synchronize(sdsp_acorr* h) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     Guard g(h->device);
+    R_TRY(h->fence.wait(), "wait for queued work");
     R_TRY(hipStreamSynchronize(h->stream), "sync");
     return SDSP_OK;
 }
@@ -426,6 +443,7 @@ struct sdsp_agc {
     bool host_valid = true;
     DevBuf d_state, d_levels, stage_in, stage_out;
     hipStream_t stream = nullptr, last = nullptr;
+    bool pipe = true;  // SDSP_TUNE_AGC_KERNEL 0
 };
 
 namespace {
@@ -518,6 +536,12 @@ void sdsp_agc_destroy(sdsp_agc* h) {
 
 size_t sdsp_agc_channels(const sdsp_agc* h) { return h ? h->channels : 0; }
 
+int sdsp_agc_set_tuning(sdsp_agc* h, int key, int value) {
+    if (!h || key != SDSP_TUNE_AGC_KERNEL || value < 0 || value > 1) return SDSP_E_INVALID_ARGUMENT;
+    h->pipe = value == 0;
+    return SDSP_OK;
+}
+
 int sdsp_agc_reset(sdsp_agc* h) {  // :178-188 (squelch stays enabled if it was on)
     return agc_update(h, [](sdsp_agc_state& s) {
         s.gain = 1.0;
@@ -534,7 +558,7 @@ int sdsp_agc_execute_block_device(sdsp_agc* h, int sample_type, const void* d_in
     Guard g(h->device);
     hipStream_t s = pick(stream, h->stream);
     if (h->last && h->last != s) R_TRY(hipStreamSynchronize(h->last), "sync");  // state hand-off between streams
-    R_TRY(launch_agc(sample_type == 1, d_in, d_out, n, h->d_state.p, h->channels, s), "agc");
+    R_TRY(launch_agc(sample_type == 1, d_in, d_out, n, h->d_state.p, h->channels, s, h->pipe), "agc");
     h->last = s;
     h->host_valid = false;
     return SDSP_OK;

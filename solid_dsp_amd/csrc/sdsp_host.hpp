@@ -110,41 +110,55 @@ struct DevBuf {
     }
 };
 
-// Completion marker of the last work a handle queued on a caller's stream.
-// *_execute_block_device may run on any stream; host-side state operations
-// (reset, set_state / get_state, clone, table rebuilds after set_scale) first
-// wait for that work, so a kernel still reading the delay line or the tables is
-// never raced by a host copy on the handle's own stream.
+// Completion marker of the last work a handle queued, on whichever stream it went
+// (a caller's stream or the handle's own).  *_execute_block_device may run on any
+// stream: each launch is first ordered after the marker (order_before) and then
+// records a new one (record), so a call on a caller stream s1, a call on the handle
+// stream and another call on s1 run in that order.  Host-side state operations
+// (reset, set_state / get_state, clone, table rebuilds after set_scale) first wait
+// for the marker, so a kernel still reading the delay line or the tables is never
+// raced by a host copy on the handle's own stream.
+//
+// The markers rotate through kRing events: a stream never re-records the event it
+// has just waited on (a stream waiting on an event that it then re-records every
+// call crashed the host side in round 3), and an event is only
+// recorded again kRing records later.
 struct StreamFence {
-    hipEvent_t ev = nullptr;
+    static constexpr int kRing = 4;
+    hipEvent_t ev[kRing] = {};
+    int cur = 0;                   // ev[cur] is the pending marker
     hipStream_t stream = nullptr;  // where the pending marker was recorded
     bool pending = false;
     StreamFence() = default;
     StreamFence(const StreamFence&) = delete;
     StreamFence& operator=(const StreamFence&) = delete;
     ~StreamFence() {
-        if (ev) (void)hipEventDestroy(ev);
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
     }
     hipError_t record(hipStream_t s) {
-        if (!ev) {
-            hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        const int nxt = (cur + 1) % kRing;
+        if (!ev[nxt]) {
+            hipError_t e = hipEventCreateWithFlags(&ev[nxt], hipEventDisableTiming);
             if (e != hipSuccess) return e;
         }
+        hipError_t e = hipEventRecord(ev[nxt], s);
+        if (e != hipSuccess) return e;
+        cur = nxt;
         pending = true;
         stream = s;
-        return hipEventRecord(ev, s);
+        return hipSuccess;
     }
-    // order work about to be queued on `s` after the pending marker; nothing to do on the
-    // marker's own stream (stream order), and the event is never waited on from the stream
-    // that re-records it
+    // order work about to be queued on `s` after the pending marker (nothing to do on the
+    // marker's own stream: stream order)
     hipError_t order_before(hipStream_t s) {
         if (!pending || s == stream) return hipSuccess;
-        return hipStreamWaitEvent(s, ev, 0);
+        return hipStreamWaitEvent(s, ev[cur], 0);
     }
     hipError_t wait() {
         if (!pending) return hipSuccess;
         pending = false;
-        return hipEventSynchronize(ev);
+        return hipEventSynchronize(ev[cur]);
     }
 };
 

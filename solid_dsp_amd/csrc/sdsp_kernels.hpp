@@ -136,6 +136,9 @@ struct FftPass {
     long long count, G, S0, S1, Si, T1, So, Ntw;
     bool inverse;
     const void* twx = nullptr;  // c32 [Tl | Th] inter-pass twiddle tables when Ntw = 2^20 (L = 1024 path)
+    int group = 4;      // generic pass: at most this many transforms per workgroup (SDSP_TUNE_FFT_GROUP)
+    int wave1024 = 16;  // L = 1024 c32 passes (SDSP_TUNE_FFT_WAVE1024): 16 pipelined persistent kernel,
+                        // 1 / 8 one-shot with 16 / 8 transforms per workgroup, 0 the generic pass
 };
 // L = 1024, complex f32 pass on the wave FFT (kern_chan1024.hip); false = not applicable
 bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err);
@@ -173,8 +176,11 @@ hipError_t launch_dot(int dtype, const DotArgs& a, hipStream_t s);
 
 // AutoCorrelator (kern_rx.hip); prec 0 = complex f32, 1 = complex f64.  hist: [channels][H]
 // oldest first (H = window size), K = max(W - delay, 0) product terms per output
+// kernel (SDSP_TUNE_ACORR_KERNEL): 0 the pipelined kernel on interior tiles where it applies, else the
+// one-shot kernel staging the delayed input in LDS; 1 the one-shot kernel everywhere (staged); 2 the
+// one-shot kernel with two loads per product (no staging)
 hipError_t launch_acorr(int prec, const void* x, const void* hist, void* y, size_t n, int H, int d, int K,
-                        size_t channels, hipStream_t s);
+                        size_t channels, hipStream_t s, int kernel = 0);
 hipError_t launch_acorr_current(int prec, const void* hist, void* out, int H, int d, int K, size_t channels,
                                 hipStream_t s);
 hipError_t launch_acorr_energy(int prec, const void* x, const void* hist, size_t n, int H, int W, size_t channels,
@@ -184,7 +190,9 @@ hipError_t launch_nco_mix(int prec, bool down, const void* x, void* y, size_t n,
                           uint32_t dtheta, int num_cus, hipStream_t s);
 // AGC bank (src/auto_gain_control/mod.rs): state is sdsp_agc_state[channels] in
 // device memory; cplx = Complex<f64> samples, else f64
-hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, size_t channels, hipStream_t s);
+// pipe: agc_pipe_kernel for calls it admits (SDSP_TUNE_AGC_KERNEL 0), else agc_kernel
+hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, size_t channels, hipStream_t s,
+                      bool pipe = true);
 hipError_t launch_agc_init(bool cplx, const void* x, size_t n, void* state, double* levels, size_t channels,
                            hipStream_t s);
 

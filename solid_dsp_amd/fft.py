@@ -51,6 +51,10 @@ class FFT:
 
     METHODS = {0: "direct DFT", 1: "Stockham (LDS)", 2: "Bluestein", 3: "four-step"}
 
+    def set_tuning(self, key: int, value: int):
+        """Kernel-variant knobs (L.TUNE_FFT_GROUP, L.TUNE_FFT_WAVE1024; performance only)."""
+        L.check(L.lib().sdsp_fft_set_tuning(self._h, int(key), int(value)))
+
     @property
     def method(self) -> str:
         """Device plan of this size (the reference plans Rader / mixed radix / DFT leaves)."""

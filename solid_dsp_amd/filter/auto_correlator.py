@@ -53,6 +53,10 @@ class AutoCorrelator:
             raise ValueError(f"expected [{self.channels}, n] samples")
         return x
 
+    def set_tuning(self, key: int, value: int):
+        """Kernel-variant knob (L.TUNE_ACORR_KERNEL; performance only, same results)."""
+        L.check(L.lib().sdsp_acorr_set_tuning(self._h, int(key), int(value)))
+
     def reset(self):  # :76-85
         L.check(L.lib().sdsp_acorr_reset(self._h))
 

@@ -116,7 +116,8 @@ def test_world2_gloo_full_gather_chunks():
 
 
 @pytest.mark.parametrize("shard", ["channel", "time"])
-@pytest.mark.parametrize("config,fault", [(2, ""), (4, ""), (2, "shift"), (4, "shift")])
+@pytest.mark.parametrize("config,fault", [(2, ""), (4, ""), (2, "shift"), (4, "shift"), (3, ""), (3, "shift"),
+                                          (5, ""), (5, "shift")])
 def test_bench_gpus2_dry_run_checks_gathered_output(config, fault, shard):
     """`bench.py --gpus 2 --dry-run` launches two ranks itself, runs the config's
     workload math per channel (the f64 restatement standing in for the device),
@@ -128,6 +129,8 @@ def test_bench_gpus2_dry_run_checks_gathered_output(config, fault, shard):
     import json
     import subprocess
     import sys
+    if config in (3, 5) and shard == "time":
+        pytest.skip("configs 3 and 5 shard by channel (stream) only")
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     env["SDSP_DRYRUN_FAULT"] = fault
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "--config",
@@ -140,7 +143,8 @@ def test_bench_gpus2_dry_run_checks_gathered_output(config, fault, shard):
     if fault:
         assert not line["gather_ok"] and line["gather_check"] > 1e-3
     else:
-        assert line["gather_ok"] and line["gather_check"] <= 1e-6
+        # configs 2 / 4 / 5: the f64 restatement stored as c32 (<= 1e-6); config 3 stores f32 (<= 1e-5)
+        assert line["gather_ok"] and line["gather_check"] <= (1e-5 if config == 3 else 1e-6)
 
 
 def test_input_windows_match_streaming_outputs():

@@ -1,29 +1,41 @@
 # In-process A/B builds of kernel variants (tools only, never shipped):
-# libsdsp_lab.so = the product objects with kern_fir_ols_os.o, kern_chan1024.o, kern_iir_wscan.o
-# rebuilt under -DSDSP_OLS_LAB -DSDSP_CHAN_LAB -DSDSP_IIR_LAB (extra template
-# instances, ablation switches: sdsp_lab_set_ols_variant, sdsp_lab_set_chan_ablation,
-# sdsp_lab_set_iir_ablation).
+# libsdsp_lab.so = the product objects, with each product TU listed in LAB_MAP
+# replaced by its lab TU under tools/lab/ (the lab TU compiles the product source
+# unchanged and adds launchers for other compile-time variants, selected by the
+# sdsp_lab_* entry points the tools/*_ab.py / *_lab.py drivers call).
 #   make -f tools/lab.mk -j8
+#   make -f tools/lab.mk archive_r03   (the frozen round-3 overlap-save lab kernels)
 HIPCC ?= /opt/rocm/bin/hipcc
 CSRC = solid_dsp_amd/csrc
 OBJ = solid_dsp_amd/_build/obj
 HIPFLAGS = --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-result \
            -fvisibility=hidden -Iinclude -I$(CSRC)
-LAB_SRC = kern_fir_ols_os kern_chan1024 kern_iir_wscan kern_pfb
+# lab TU : the product object it replaces
+LAB_MAP = ols_lab:kern_fir_ols_os chan_lab:kern_chan1024 iir_lab:kern_iir_wscan
+LAB_TUS = $(foreach m,$(LAB_MAP),$(word 1,$(subst :, ,$(m))))
+REPLACED = $(foreach m,$(LAB_MAP),$(OBJ)/$(word 2,$(subst :, ,$(m))).o)
 OUT = tools/_build/libsdsp_lab.so
-PRODUCT_OBJS = $(filter-out $(patsubst %,$(OBJ)/%.o,$(LAB_SRC)),$(wildcard $(OBJ)/*.o))
+PRODUCT_OBJS = $(filter-out $(REPLACED),$(wildcard $(OBJ)/*.o))
 
 all: $(OUT)
 
-tools/_build/lab/%.o: $(CSRC)/%.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
+tools/_build/lab/%.o: tools/lab/%.hip $(CSRC)/*.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
 	@mkdir -p tools/_build/lab
-	$(HIPCC) $(HIPFLAGS) -DSDSP_OLS_LAB -DSDSP_CHAN_LAB -DSDSP_IIR_LAB -DSDSP_PFB_LAB -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-# the slot kernel's queue atomic is issued by one lane and its result is needed a segment later: no
-# wave-level atomic rewrite (it waits for the returned value at once)
-tools/_build/lab/kern_fir_ols_os.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+tools/_build/lab/iir_lab.o: HIPFLAGS += -fno-slp-vectorize
 
-tools/_build/lab/kern_iir_wscan.o: HIPFLAGS += -fno-slp-vectorize
-
-$(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_SRC)) $(PRODUCT_OBJS)
+$(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_TUS)) $(PRODUCT_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^
+
+# round-3 archive: the slot / pair / trio / quad / queue kernels (sdsp_lab_set_ols_variant
+# variants >= 256 of that round)
+ARCH_OUT = tools/_build/libsdsp_lab_r03.so
+ARCH_KEEP = $(filter-out $(OBJ)/kern_fir_ols_os.o,$(wildcard $(OBJ)/*.o))
+tools/_build/lab/kern_fir_ols_os_r03.o: tools/lab/archive_r03/kern_fir_ols_os_r03.hip
+	@mkdir -p tools/_build/lab
+	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-atomic-optimizer-strategy=None -c $< -o $@
+archive_r03: tools/_build/lab/kern_fir_ols_os_r03.o
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $(ARCH_OUT) $< $(ARCH_KEEP)
+
+.PHONY: all archive_r03

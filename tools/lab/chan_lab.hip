@@ -1,0 +1,32 @@
+// Lab translation unit for the streaming channeliser (tools only, never part of
+// libsdsp.so): the product source compiled unchanged (its launcher renamed) plus
+// a launcher that runs chan1024_kernel<..., LAB> for the LAB value set by
+// sdsp_lab_set_chan_ablation (tools/chan_ab.py).  LAB bits are documented at
+// chan1024_kernel.  tools/lab.mk links it in place of the product object.
+#define try_launch_chan1024 try_launch_chan1024_product
+#include "kern_chan1024.hip"
+#undef try_launch_chan1024
+
+namespace sdsp {
+
+static int g_chan_lab = 0;
+
+bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
+    switch (g_chan_lab) {
+        case 1: return try_launch_chan1024_t<1>(a, s, err);
+        case 2: return try_launch_chan1024_t<2>(a, s, err);
+        case 4: return try_launch_chan1024_t<4>(a, s, err);
+        case 6: return try_launch_chan1024_t<6>(a, s, err);
+        case 32: return try_launch_chan1024_t<32>(a, s, err);
+        case 64: return try_launch_chan1024_t<64>(a, s, err);
+        default: return try_launch_chan1024_t<0>(a, s, err);
+    }
+}
+
+}  // namespace sdsp
+
+// tools/chan_ab.py encoding: 1 no FFT, 2 no loads, 4 no stores, 8 plain stores,
+// 16 nontemporal loads, 32 / 64 odd workgroups start ~6.8 / ~3.4 us late
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) {
+    sdsp::g_chan_lab = (v & 7) | ((v >> 2) & 24) | ((v & 8) ? 32 : 0) | ((v & 16) ? 64 : 0);
+}

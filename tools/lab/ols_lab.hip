@@ -1,0 +1,33 @@
+// Lab translation unit for the one-shot overlap-save kernel (tools only, never
+// part of libsdsp.so).  It compiles the product source unchanged, renaming its
+// launcher, and adds a launcher that runs other compile-time variants
+// (fir_ols_os_kernel<ABL>, bits documented at ols_os_segment) selected by
+// sdsp_lab_set_ols_variant -- the in-process A/B driver is tools/ols_lab.py.
+// tools/lab.mk links it in place of the product object.
+#define launch_fir_ols_os launch_fir_ols_os_product
+#include "kern_fir_ols_os.hip"
+#undef launch_fir_ols_os
+
+namespace sdsp {
+
+static int g_lab_variant = 0, g_lab_lds = 0;
+
+#define SDSP_OLS_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(128) X(132) X(256) X(260)
+
+hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
+                             long long lo, long long hi) {
+#define SDSP_OLS_LAB_CASE(V) \
+    if (g_lab_variant == V) return launch_fir_ols_os_t<V>(p, x, y, n, channels, s, lo, hi, (size_t)g_lab_lds);
+    SDSP_OLS_LAB_VARIANTS(SDSP_OLS_LAB_CASE)
+#undef SDSP_OLS_LAB_CASE
+    return launch_fir_ols_os_t<0>(p, x, y, n, channels, s, lo, hi, (size_t)g_lab_lds);
+}
+
+}  // namespace sdsp
+
+// variant (ABL bits), dynamic LDS bytes (pins occupancy); the third argument is unused
+// (kept for tools/ols_lab.py)
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_ols_variant(int v, int lds, int) {
+    sdsp::g_lab_variant = v;
+    sdsp::g_lab_lds = lds;
+}
