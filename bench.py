@@ -254,8 +254,27 @@ class Cfg3IIR:
                            algo=sd.ALGO_FMA)
         self.d_in = torch.empty(self.n, dtype=torch.float32, device="cuda")
         self.d_out = torch.empty(self.n, dtype=torch.float32, device="cuda")
-        sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, self.n,
-                                       torch.cuda.current_stream().cuda_stream)
+        self.shard = getattr(args, "shard", "channel")
+        self.rank = rank
+        cs = torch.cuda.current_stream().cuda_stream
+        if self.shard == "time":
+            # segment `rank` of ONE stream (channel 0), joined to the segments before it by one
+            # exchange of the boundary states (parallel.iir_exclusive_scan)
+            from solid_dsp_amd import parallel as P
+            sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, 0, rank * self.n, self.n, cs)
+            A, _, c, _ = P.sos_state_space(self.ff, self.fb)
+            self.Phi = P.state_transition(A, self.n)
+            self.W = P.zero_input_length(A, c, self.n)
+            self.g = IIRFilter(self.ff, self.fb, IIRFilterType.SecondOrder, sample_dtype=np.float32, device=dev,
+                               algo=sd.ALGO_FMA)
+            self.d_zero = torch.zeros(self.W, dtype=torch.float32, device="cuda")
+            self.d_corr = torch.empty(self.W, dtype=torch.float32, device="cuda")
+            self.parallelism = ("one stream (channel 0) time-sharded: rank r filters inputs [r n, (r+1) n) from zero "
+                                "state, one all_gather of the 8 boundary-state values, exclusive scan of the states "
+                                f"and the zero-input response of the true initial state added to the first {self.W} "
+                                "outputs")
+        else:
+            sd.lib().sdsp_synth_f32_device(self.d_in.data_ptr(), SEED, rank, 0, self.n, cs)
         self.samples_per_step = self.n
         self.bytes_per_step = 8 * self.n
         self.dtype = "f32 (f32 coefficients, real f32 samples)"
@@ -264,11 +283,26 @@ class Cfg3IIR:
         self.algo_name = "scan"
 
     def step(self, stream):
+        if self.shard != "time":
+            self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+            return
+        # time shard: the segment from zero state, the boundary-state exchange, the correction
+        import torch
+        from solid_dsp_amd import parallel as P
+        self.f.reset()  # every timed step re-runs the same segment from zero state
         self.f.execute_block_device(self.d_in, self.n, self.d_out, stream)
+        s_r, _ = self.f.get_state()  # waits for the block
+        init = P.iir_exclusive_scan(P.exchange_states(s_r.astype(np.float64), device="cuda"), self.Phi)[self.rank]
+        self.g.set_state(init.astype(np.float32))
+        self.g.execute_block_device(self.d_zero, self.W, self.d_corr, stream)
+        with torch.cuda.stream(stream):
+            self.d_out[: self.W] += self.d_corr
 
     def parity(self, stream, rng):
         import oracle_lib as O
         import torch
+        if self.shard == "time" and self.rank != 0:
+            return None  # rank 0 holds the stream's start; the gathered check covers the others
         m = 1 << 20  # the first 2^20 outputs of a fresh pass vs the f64 restatement (IIR: full prefix)
         from solid_dsp_amd import IIRFilter, IIRFilterType
         import solid_dsp_amd as sd
@@ -305,6 +339,11 @@ class Cfg3IIR:
         return P.check_gathered(big, lambda r, s, w: Cfg3IIR.expected(ff, fb, r, s, w), rng, width, 0, n)
 
     def check_gathered(self, big, rng, width=4096):
+        """channel shards: two random windows of every rank's channel; time shards: windows of
+        the one stream inside every segment and across every segment boundary"""
+        from solid_dsp_amd import parallel as P
+        if self.shard == "time":
+            return P.check_time_sharded(big, lambda g, w: Cfg3IIR.expected(self.ff, self.fb, 0, g, w), rng, width, 0)
         return Cfg3IIR.check(big, self.ff, self.fb, self.n, rng, width)
 
     def cpu(self, samples):
@@ -1070,7 +1109,20 @@ def dry_run(args, rank, world):
         expected = lambda r, m, w: Cfg4Decim.expected(h, r, m, w)
         lo, hi, width = 8, n // 32, 256
     t0 = time.perf_counter()
-    if cfg == 3:
+    if cfg == 3 and args.shard == "time":  # segment `rank` of one stream, one state exchange
+        A3, _, c3, _ = P.sos_state_space(ff, fb)
+        o = O.iir(O.RR64, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER)
+        y0 = o.execute_block(O.synth(SEED, 0, rank * n, n).astype(np.float64))
+        states = P.exchange_states(o.sos_state())
+        init = P.iir_exclusive_scan(states, P.state_transition(A3, n))[rank]
+        if os.environ.get("SDSP_DRYRUN_FAULT") == "noexchange":
+            init = np.zeros_like(init)
+        g3 = O.iir(O.RR64, ff.astype(np.float64), fb.astype(np.float64), O.SECOND_ORDER)
+        g3.sos_state(init)
+        W3 = P.zero_input_length(A3, c3, n)
+        y0[:W3] += g3.execute_block(np.zeros(W3))
+        y = y0.astype(np.float32)
+    elif cfg == 3:
         y = run(O.synth(SEED, rank, 0, n).astype(np.float64)).astype(np.float32)
     elif cfg == 5:
         y = run5(rank).astype(np.complex64)
@@ -1086,7 +1138,10 @@ def dry_run(args, rank, world):
     ranks = P.gather_to_root(torch.tensor([rank], dtype=torch.int64), 0)
     big = P.gather_full_to_root(torch.from_numpy(y), 0, chunk_bytes=1 << 14)
     if rank == 0:
-        if cfg in (3, 5):
+        if cfg == 3 and args.shard == "time":
+            worst = P.check_time_sharded(big, lambda g, w: Cfg3IIR.expected(ff, fb, 0, g, w),
+                                         np.random.default_rng(2), 2048, 0)
+        elif cfg in (3, 5):
             worst = check(big, np.random.default_rng(2))
         elif args.shard == "time":
             worst = P.check_time_sharded(big, lambda g, w: expected(0, g, w), np.random.default_rng(2), width, lo)
@@ -1109,8 +1164,8 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     if args.gpus is not None and args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.shard == "time" and args.config not in (2, 4):
-        sys.exit("bench.py: --shard time applies to configs 2 (FIR) and 4 (decimator)")
+    if args.shard == "time" and args.config not in (2, 3, 4):
+        sys.exit("bench.py: --shard time applies to configs 2 (FIR), 3 (IIR) and 4 (decimator)")
     if args.dry_run:
         return dry_run(args, rank, world)
 

@@ -196,6 +196,9 @@ struct Obj {
     virtual double group_delay(double) { return 0.0; }
     virtual cpx<double> frequency_response(double) { return {0.0, 0.0}; }
     virtual Obj* clone() const = 0;
+    // SecondOrder IIR state (w1, w2) per section, the device handle's layout (sdsp_iir_get_state):
+    // copied to st (set = 0) or from st (set = 1) as the sample type; 1 = not an SOS cascade
+    virtual int sos_state(void*, int) { return 1; }
 };
 
 // FIRFilter<Coef,In>  src/filter/fir/mod.rs:58-304
@@ -417,6 +420,23 @@ template <typename C, typename I> struct IIR : Obj {
         return d;
     }
     Obj* clone() const override { return new IIR(*this); }
+    // the delay line of section q after a step is [w, w1_old, w2_old] newest first: the state the
+    // next step reads is (buf[0], buf[1]) (sos.rs:92-114; buf[2] is overwritten before use)
+    int sos_state(void* st, int set) override {
+        if (type != SECOND_ORDER) return 1;
+        I* p = (I*)st;
+        for (size_t q = 0; q < sections.size(); ++q) {
+            auto& b = sections[q].wbuf.buf;
+            if (set) {
+                b[0] = p[2 * q];
+                b[1] = p[2 * q + 1];
+            } else {
+                p[2 * q] = b[0];
+                p[2 * q + 1] = b[1];
+            }
+        }
+        return 0;
+    }
 };
 
 // DecimatingIIRFilter  src/filter/iir/decim.rs:190-233
@@ -517,6 +537,7 @@ void orc_write(void* h, const void* x, size_t n) { ((Obj*)h)->write(x, n); }
 void orc_reset(void* h) { ((Obj*)h)->reset(); }
 void* orc_clone(void* h) { return ((Obj*)h)->clone(); }
 void orc_free(void* h) { delete (Obj*)h; }
+int orc_sos_state(void* h, void* st, int set) { return ((Obj*)h)->sos_state(st, set); }
 double orc_group_delay(void* h, double f) { return ((Obj*)h)->group_delay(f); }
 void orc_frequency_response(void* h, double f, double* out2) {
     cpx<double> r = ((Obj*)h)->frequency_response(f);

@@ -82,7 +82,7 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // (never part of libsdsp.so).  Bits: 1 block barriers at the wave-local phase
 // boundaries; 2 no HBM traffic (ablation: outputs dropped); 4 HBM traffic only
 // (ablation: no transform); 128 plain (not nontemporal) stores; 256 input rows
-// loaded last to first.
+// loaded last to first; 512 output rows stored last to first.
 template <int ABL>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -101,10 +101,12 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     }
     if constexpr (ABL & 4) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
+        for (int i = 0; i < 16; ++i) {
+            const int r = (ABL & 512) ? 15 - i : i;
             if (r >= h2)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[r]), ry, 8 * t, 2048 * r,
                                                       (ABL & 128) ? 0 : 2);
+        }
         return;
     }
     // twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build)
@@ -184,9 +186,11 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     // nontemporal stores (3.14 -> 3.08 ms on cfg2, in-process A/B)
     constexpr int kStAux = (ABL & 128) ? 0 : 2;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
+    for (int i = 0; i < 16; ++i) {
+        const int r = (ABL & 512) ? 15 - i : i;
         if (r >= h2)
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, kStAux);
+    }
 }
 
 template <int ABL>

@@ -32,6 +32,10 @@ class DotProduct:
         self.dtype = L.dtype_code(self._c.dtype, sample_dtype)
         self.sample_dtype = L.SAMPLE_DTYPE[self.dtype]
 
+    @classmethod
+    def new(cls, coefficients, direction, **kw):  # DotProduct::new  mod.rs:57-87
+        return cls(coefficients, direction, **kw)
+
     def coefficents(self) -> np.ndarray:  # sic (mod.rs:102-109): stored order
         return self._c[::-1].copy() if self.direction == Direction.REVERSE else self._c.copy()
 

@@ -196,6 +196,10 @@ class DecimatingIIRFilter(_IirBase):
     def __init__(self, feed_forward, feed_back, iirtype, decimation, **kw):
         super().__init__(feed_forward, feed_back, iirtype, decimation, **kw)
 
+    @classmethod
+    def new(cls, feed_forward, feed_back, iirtype, decimation, **kw):  # decim.rs:11-30
+        return cls(feed_forward, feed_back, iirtype, decimation, **kw)
+
     def get_decimation(self):
         return self._factor
 
@@ -207,6 +211,10 @@ class InterpolatingIIRFilter(_IirBase):
 
     def __init__(self, feed_forward, feed_back, iirtype, interpolation, **kw):
         super().__init__(feed_forward, feed_back, iirtype, interpolation, **kw)
+
+    @classmethod
+    def new(cls, feed_forward, feed_back, iirtype, interpolation, **kw):  # interp.rs:12-31
+        return cls(feed_forward, feed_back, iirtype, interpolation, **kw)
 
     def get_interpolation(self):
         return self._factor
@@ -229,6 +237,13 @@ class SecondOrderFilter:
         self._f.iirtype = IIRFilterType.SecondOrder
         self._f.channels = 1
         self._f._factor = 1
+
+    @classmethod
+    def new(cls, feed_forward, feed_back, coef_dtype=np.float64, sample_dtype=np.float64, **kw):  # sos.rs:55-75
+        """SecondOrderFilter::<f64, f64>::new -- the only instantiation the reference's bounds admit"""
+        if np.dtype(coef_dtype) != np.float64 or np.dtype(sample_dtype) != np.float64:
+            raise TypeError("SecondOrderFilter is SecondOrderFilter<f64, f64>")
+        return cls(feed_forward, feed_back, **kw)
 
     def execute(self, sample: float) -> float:  # sos.rs:92-114 (Left(input))
         return float(self._f.execute(sample)[0])

@@ -181,3 +181,116 @@ def check_time_sharded(big, expected, rng, width: int, lo: int, windows: int = 2
             return float("inf")
         worst = max(worst, float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-300)))
     return worst
+
+
+# ---------------------------------------------------------------------------
+# Time-sharding one IIR stream ("one exchange step: an exclusive scan of
+# the 2 S-dim boundary state").  The SOS cascade carries D = 2 S state values across
+# a cut -- (w1, w2) of every section, src/filter/iir/sos.rs:92-114, in the device
+# handle's layout -- so segments are not independent.  Rank r runs its segment
+# x[r n, (r + 1) n) from zero state (outputs y0_r, final state s_r); the ranks
+# exchange the s_r (one all_gather of D values each); every rank forms the exclusive
+# scan  I_0 = st0,  I_{r+1} = Phi I_r + s_r  with Phi = A^n (the state transition
+# over one segment), and adds the zero-input response of its true initial state:
+#     y_r[i] = y0_r[i] + c A^i I_r,
+# computed by a second handle set to state I_r over i < W zeros, where W is where
+# c A^i has decayed below rounding (the whole segment when it does not decay).
+# Exact up to rounding for every cascade, decaying or not; the exchange is D values.
+
+def sos_state_space(ff, fb):
+    """(A, b, c, d) of an SOS cascade in f64, state S = [w1_0, w2_0, w1_1, w2_1, ...]:
+    S' = A S + b x, y = c S + d x, with the coefficients normalised by a0 as
+    SecondOrderFilter::new does (sos.rs:55-75) and the recurrence of sos.rs:92-114
+    (section q feeds section q + 1, iir/mod.rs:281-287)."""
+    import numpy as np
+    ff = np.asarray(ff, np.float64).reshape(-1, 3)
+    fb = np.asarray(fb, np.float64).reshape(-1, 3)
+    S = len(ff)
+    D = 2 * S
+
+    def step(st, x):
+        st = st.copy()
+        v = x
+        for q in range(S):
+            a0 = fb[q, 0]
+            b0, b1, b2 = ff[q] / a0
+            a1, a2 = fb[q, 1] / a0, fb[q, 2] / a0
+            w1, w2 = st[2 * q], st[2 * q + 1]
+            w = v - (a1 * w1 + a2 * w2)
+            v = b0 * w + b1 * w1 + b2 * w2
+            st[2 * q + 1] = w1
+            st[2 * q] = w
+        return st, v
+
+    A = np.zeros((D, D))
+    c = np.zeros(D)
+    for j in range(D):
+        e = np.zeros(D)
+        e[j] = 1.0
+        A[:, j], c[j] = step(e, 0.0)
+    b, d = step(np.zeros(D), 1.0)
+    return A, b, c, d
+
+
+def state_transition(A, n: int):
+    """A^n in f64 by repeated squaring"""
+    import numpy as np
+    R = np.eye(A.shape[0])
+    P = np.array(A, np.float64)
+    while n:
+        if n & 1:
+            R = P @ R
+        P = P @ P
+        n >>= 1
+    return R
+
+
+def iir_exclusive_scan(states, Phi, st0=None):
+    """I_0 = st0 (zero state when None), I_{r+1} = Phi I_r + states[r]: the true initial
+    state of every segment from the segments' zero-state final states"""
+    import numpy as np
+    D = Phi.shape[0]
+    cur = np.zeros(D, dtype=np.result_type(np.asarray(states).dtype, np.float64)) if st0 is None else \
+        np.asarray(st0, dtype=np.result_type(np.asarray(st0).dtype, np.float64))
+    out = []
+    for s in states:
+        out.append(cur.copy())
+        cur = Phi @ cur + np.asarray(s)
+    return out
+
+
+def zero_input_length(A, c, n: int, rel: float = 1e-12) -> int:
+    """samples after which the zero-input response c A^i I is below `rel` of its peak gain
+    (rounded up to 4096, at most n); n when it does not decay within n samples"""
+    import numpy as np
+    g = np.array(c, np.float64)
+    peak = max(np.abs(g).sum(), 1e-300)
+    i = 0
+    while i < n:
+        if np.abs(g).sum() <= rel * peak and i > 0:
+            return min(n, -(-i // 4096) * 4096)
+        g = g @ A
+        i += 1
+        peak = max(peak, np.abs(g).sum())
+    return n
+
+
+def exchange_states(state, device=None):
+    """all_gather of every rank's D-value state (complex as (re, im) pairs) in f64: the
+    one collective of the IIR time shard"""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    s = np.asarray(state)
+    cplx = np.iscomplexobj(s)
+    flat = np.stack([s.real, s.imag], -1).reshape(-1) if cplx else s.astype(np.float64)
+    t = torch.tensor(np.asarray(flat, np.float64), device=device)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        parts = [t]
+    else:
+        parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, t)
+    out = [p.cpu().numpy() for p in parts]
+    if cplx:
+        out = [o.reshape(-1, 2) @ np.array([1.0, 1.0j]) for o in out]
+    return out

@@ -51,6 +51,7 @@ def lib():
         "orc_reset": (None, [vp]),
         "orc_clone": (vp, [vp]),
         "orc_free": (None, [vp]),
+        "orc_sos_state": (C.c_int, [vp, vp, C.c_int]),
         "orc_group_delay": (C.c_double, [vp, C.c_double]),
         "orc_frequency_response": (None, [vp, C.c_double, dp]),
         "orc_pfb_execute": (C.c_int, [vp, C.c_int, sz, vp]),
@@ -191,6 +192,17 @@ class OracleObj:
         lib().orc_frequency_response(self.h, f, _dptr(out))
         return complex(out[0], out[1])
 
+    def sos_state(self, state=None):
+        """SecondOrder IIR: the (w1, w2) state per section in the device handle's layout;
+        with `state`, set it instead"""
+        n = 2 * self._sections
+        if state is None:
+            st = np.zeros(n, dtype=self.in_dt)
+            assert lib().orc_sos_state(self.h, _ptr(st), 0) == 0
+            return st
+        st = np.ascontiguousarray(state, dtype=self.in_dt)
+        assert lib().orc_sos_state(self.h, _ptr(st), 1) == 0
+
     def pfb_execute(self, index):
         out = np.zeros(1, dtype=self.in_dt)
         rc = lib().orc_pfb_execute(self.h, self.dtype, index, _ptr(out))
@@ -233,7 +245,9 @@ def interp(dtype, taps, M):
 def iir(dtype, ff, fb, type_):
     a = np.ascontiguousarray(ff, dtype=_COEF_DT[dtype])
     b = np.ascontiguousarray(fb, dtype=_COEF_DT[dtype])
-    return OracleObj(_mk(lib().orc_iir_new, dtype, _ptr(a), len(a), _ptr(b), len(b), type_), dtype, kind="iir")
+    o = OracleObj(_mk(lib().orc_iir_new, dtype, _ptr(a), len(a), _ptr(b), len(b), type_), dtype, kind="iir")
+    o._sections = len(a) // 3
+    return o
 
 
 def iir_decim(dtype, ff, fb, type_, M):

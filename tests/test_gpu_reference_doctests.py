@@ -1,0 +1,543 @@
+"""The reference's doctests of the hot path (juliantos/solid-dsp src/filter/{fir,iir}/*.rs,
+src/dot_product/*.rs), translated statement by statement by tools/port_doctests.py to the
+Python mirror of the C ABI (solid_dsp_amd) and run on the MI355X: every call goes through
+libsdsp.so, and each asserted literal is the reference's, compared exactly as Rust's
+assert_eq! compares (f64 / Complex<f64> equality).  Generated -- edit the porter, not this file."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+sd = pytest.importorskip("solid_dsp_amd")
+from solid_dsp_amd import (FIRFilter, DecimatingFIRFilter, InterpolatingFIRFilter, PolyPhaseFilterBank,  # noqa
+                           IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter, InterpolatingIIRFilter,
+                           DotProduct, Direction)
+from solid_dsp_amd.filter import firdes, iirdes  # noqa: E402
+from solid_dsp_amd.filter.firdes import *  # noqa: E402,F401,F403
+
+
+def _plain(v):
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, (list, tuple)):
+        return [_plain(u) for u in v]
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def _eq(a, b):
+    """assert_eq!: exact equality, element by element for sequences"""
+    pa, pb = _plain(a), _plain(b)
+    assert pa == pb, (pa, pb)
+
+
+def _len(x):
+    return x.len() if hasattr(x, "len") and callable(x.len) else len(x)
+
+
+def _round(v):  # f64::round: half away from zero
+    return math.floor(v + 0.5) if v >= 0 else -math.floor(-v + 0.5)
+
+
+def test_filter_fir_mod_l73():
+    """src/filter/fir/mod.rs:73"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+
+
+def test_filter_fir_mod_l96():
+    """src/filter/fir/mod.rs:96"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter.set_scale(2.0)
+    _eq(filter.get_scale(), 2.0)
+
+
+def test_filter_fir_mod_l116():
+    """src/filter/fir/mod.rs:116"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.get_scale(), 1.0)
+
+
+def test_filter_fir_mod_l132():
+    """src/filter/fir/mod.rs:132"""
+    coefs = [0.0] * 12
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    len = _len(filter)
+    _eq(len, 12)
+
+
+def test_filter_fir_mod_l150():
+    """src/filter/fir/mod.rs:150"""
+    coefs = [0.0] * 12
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.is_empty(), False)
+
+
+def test_filter_fir_mod_l166():
+    """src/filter/fir/mod.rs:166"""
+    coefs = [0.0] * 12
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    ref_coefs = filter.coefficients()
+    _eq(coefs, ref_coefs)
+
+
+def test_filter_fir_mod_l195():
+    """src/filter/fir/mod.rs:195"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    window = [complex(2.02, 0.0), complex(4.04, 0.0), complex(1.02, 0.0), complex(0.23, 0.0), complex(9.19, 0.0)]
+    output = filter.execute(window[0])
+    _eq(output[0], complex(10.1, 0.0))
+
+
+def test_filter_fir_mod_l221():
+    """src/filter/fir/mod.rs:221"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    window = [complex(2.02, 0.0), complex(4.04, 0.0), complex(1.02, 0.0), complex(0.23, 0.0), complex(9.19, 0.0)]
+    output = filter.execute_block(window)
+    _eq(output[4], complex(60.03, 0.0))
+
+
+def test_filter_fir_mod_l247():
+    """src/filter/fir/mod.rs:247"""
+    coefs = firdes_notch(25, 0.35, 120.0)
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.float64)
+    response = filter.frequency_response(0.0)
+    _eq(_round(response.real), 1.0)
+    _eq(response.imag, 0.0)
+
+
+def test_filter_fir_mod_l279():
+    """src/filter/fir/mod.rs:279"""
+    coefs = firdes.firdes_notch(12, 0.35, 120.0)
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.float64)
+    delay = filter.group_delay(0.0)
+    _eq(int(delay + 0.5), 12)
+
+
+def test_filter_fir_decim_l21():
+    """src/filter/fir/decim.rs:21"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+
+
+def test_filter_fir_decim_l50():
+    """src/filter/fir/decim.rs:50"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter.set_scale(2.0)
+    _eq(filter.get_scale(), 2.0)
+
+
+def test_filter_fir_decim_l70():
+    """src/filter/fir/decim.rs:70"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.get_scale(), 1.0)
+
+
+def test_filter_fir_decim_l88():
+    """src/filter/fir/decim.rs:88"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.get_decimation(), 2)
+
+
+def test_filter_fir_decim_l106():
+    """src/filter/fir/decim.rs:106"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter.push(complex(4.0, 0.0))
+
+
+def test_filter_fir_decim_l126():
+    """src/filter/fir/decim.rs:126"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    window = [complex(2.02, 0.0), complex(4.04, 0.0)]
+    filter.write(window)
+
+
+def test_filter_fir_decim_l145():
+    """src/filter/fir/decim.rs:145"""
+    coefs = [0.0] * 12
+    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    len = _len(filter)
+    _eq(len, 12)
+
+
+def test_filter_fir_decim_l163():
+    """src/filter/fir/decim.rs:163"""
+    coefs = [0.0] * 12
+    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.is_empty(), False)
+
+
+def test_filter_fir_decim_l179():
+    """src/filter/fir/decim.rs:179"""
+    coefs = [0.0] * 12
+    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    ref_coefs = filter.coefficients()
+    _eq(coefs, ref_coefs)
+
+
+def test_filter_fir_decim_l208():
+    """src/filter/fir/decim.rs:208"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    window = [complex(2.02, 0.0), complex(4.04, 0.0)]
+    first_output = filter.execute(window[0])
+    second_output = filter.execute(window[1])
+    _eq(first_output, [])
+    _eq(second_output, [complex(28.28, 0.0)])
+
+
+def test_filter_fir_decim_l237():
+    """src/filter/fir/decim.rs:237"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    window = [complex(2.02, 0.0), complex(4.04, 0.0), complex(1.02, 0.0), complex(0.23, 0.0)]
+    output = filter.execute_block(window)
+    _eq(output, [complex(28.28, 0.0), complex(21.39, 0.0)])
+
+
+def test_filter_fir_interp_l21():
+    """src/filter/fir/interp.rs:21"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = InterpolatingFIRFilter.new(coefficients, 4, coef_dtype=np.float64, sample_dtype=np.complex128)
+
+
+def test_filter_fir_pfb_l18():
+    """src/filter/fir/pfb.rs:18"""
+    coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
+    filter = PolyPhaseFilterBank.new(coefficients, 2, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+
+
+def test_filter_iir_mod_l84():
+    """src/filter/iir/mod.rs:84"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder, coef_dtype=np.float64, sample_dtype=np.complex128)
+
+
+def test_filter_iir_mod_l170():
+    """src/filter/iir/mod.rs:170"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder, coef_dtype=np.float64, sample_dtype=np.float64)
+    numerators = iir_filter.numerator_coefs()
+    _eq(numerators, filter[0])
+
+
+def test_filter_iir_mod_l190():
+    """src/filter/iir/mod.rs:190"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder, coef_dtype=np.float64, sample_dtype=np.float64)
+    denominators = iir_filter.denominator_coefs()
+    _eq(denominators, filter[1])
+
+
+def test_filter_iir_mod_l210():
+    """src/filter/iir/mod.rs:210"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder, coef_dtype=np.float64, sample_dtype=np.float64)
+    filters = iir_filter.second_order_filters()
+    _eq(_len(filters), 1)
+
+
+def test_filter_iir_mod_l230():
+    """src/filter/iir/mod.rs:230"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder, coef_dtype=np.float64, sample_dtype=np.float64)
+    _eq(iir_filter.iir_type(), IIRFilterType.SecondOrder)
+
+
+def test_filter_iir_mod_l257():
+    """src/filter/iir/mod.rs:257"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder)
+    output = iir_filter.execute(1.0)
+    _eq(output[0], 0.05816769596076701)
+
+
+def test_filter_iir_mod_l297():
+    """src/filter/iir/mod.rs:297"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder)
+    output = iir_filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    _eq(output, [0.05816769596076701, 0.119535296293297, 0.18410279587774706, 0.2518701895942824, 0.32283747232307686])
+
+
+def test_filter_iir_mod_l322():
+    """src/filter/iir/mod.rs:322"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder)
+    output = iir_filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    freq_res = iir_filter.frequency_response(0.0)
+    _eq(freq_res, complex(0.0, 0.0))
+
+
+def test_filter_iir_mod_l378():
+    """src/filter/iir/mod.rs:378"""
+    filter = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    iir_filter = IIRFilter.new(filter[0], filter[1], IIRFilterType.SecondOrder)
+    output = iir_filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    delay = iir_filter.group_delay(0.0)
+    _eq(delay, 19.6774211296624)
+
+
+def test_filter_iir_sos_l48():
+    """src/filter/iir/sos.rs:48"""
+    ff_coefs, fb_coefs = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    second_order_filter = SecondOrderFilter.new(ff_coefs, fb_coefs, coef_dtype=np.float64, sample_dtype=np.float64)
+
+
+def test_filter_iir_sos_l81():
+    """src/filter/iir/sos.rs:81"""
+    ff_coefs, fb_coefs = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    second_order_filter = SecondOrderFilter.new(ff_coefs, fb_coefs, coef_dtype=np.float64, sample_dtype=np.float64)
+    output = second_order_filter.execute((1.0))
+    _eq(output, 0.05816769596076701)
+
+
+def test_filter_iir_sos_l120():
+    """src/filter/iir/sos.rs:120"""
+    ff_coefs, fb_coefs = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    second_order_filter = SecondOrderFilter.new(ff_coefs, fb_coefs, coef_dtype=np.float64, sample_dtype=np.float64)
+    numerators = second_order_filter.numerator_coefs()
+    _eq(_len(numerators), 2)
+    _eq(numerators[1], 0.99999840000128)
+
+
+def test_filter_iir_sos_l140():
+    """src/filter/iir/sos.rs:140"""
+    ff_coefs, fb_coefs = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    second_order_filter = SecondOrderFilter.new(ff_coefs, fb_coefs, coef_dtype=np.float64, sample_dtype=np.float64)
+    denominators = second_order_filter.denominator_coefs()
+    _eq(_len(denominators), 3)
+    _eq(denominators[1], 0.003199997440002048)
+
+
+def test_filter_iir_sos_l160():
+    """src/filter/iir/sos.rs:160"""
+    ff_coefs, fb_coefs = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    second_order_filter = SecondOrderFilter.new(ff_coefs, fb_coefs, coef_dtype=np.float64, sample_dtype=np.float64)
+    freq_res = second_order_filter.frequency_response(0.0)
+    assert freq_res != complex(0.0, 0.0)
+
+
+def test_filter_iir_sos_l197():
+    """src/filter/iir/sos.rs:197"""
+    ff_coefs, fb_coefs = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    second_order_filter = SecondOrderFilter.new(ff_coefs, fb_coefs, coef_dtype=np.float64, sample_dtype=np.float64)
+    delay = second_order_filter.group_delay(0.0)
+    _eq(delay, 17.6774211296624)
+
+
+def test_filter_iir_decim_l21():
+    """src/filter/iir/decim.rs:21"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+
+
+def test_filter_iir_decim_l53():
+    """src/filter/iir/decim.rs:53"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.get_decimation(), 2)
+
+
+def test_filter_iir_decim_l72():
+    """src/filter/iir/decim.rs:72"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    numerators = filter.numerator_coefs()
+    orig_ratio = coefficients[0][0] / coefficients[0][1]
+    new_ratio = numerators[0] / numerators[1]
+    _eq(orig_ratio, new_ratio)
+
+
+def test_filter_iir_decim_l96():
+    """src/filter/iir/decim.rs:96"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    denominators = filter.denominator_coefs()
+    orig_ratio = coefficients[1][0] / coefficients[1][1]
+    new_ratio = denominators[1] / denominators[0]
+    assert abs(orig_ratio - new_ratio) < 0.00001
+
+
+def test_filter_iir_decim_l120():
+    """src/filter/iir/decim.rs:120"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filters = filter.second_order_filters()
+    _eq(_len(filters), 1)
+
+
+def test_filter_iir_decim_l142():
+    """src/filter/iir/decim.rs:142"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.iir_type(), IIRFilterType.SecondOrder)
+
+
+def test_filter_iir_decim_l174():
+    """src/filter/iir/decim.rs:174"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2)
+    output = filter.execute(0.0)
+    _eq(output, [])
+    output = filter.execute(1.0)
+    _eq(output[0], 0.05816769596076701)
+
+
+def test_filter_iir_decim_l207():
+    """src/filter/iir/decim.rs:207"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2)
+    output = filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    _eq(output, [0.119535296293297, 0.2518701895942824])
+
+
+def test_filter_iir_decim_l239():
+    """src/filter/iir/decim.rs:239"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2)
+    output = filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    freq_res = filter.frequency_response(0.0)
+    _eq(freq_res, complex(0.0, 0.0))
+
+
+def test_filter_iir_decim_l262():
+    """src/filter/iir/decim.rs:262"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = DecimatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2)
+    output = filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    delay = filter.group_delay(0.0)
+    _eq(delay, 19.6774211296624)
+
+
+def test_filter_iir_interp_l20():
+    """src/filter/iir/interp.rs:20"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+
+
+def test_filter_iir_interp_l51():
+    """src/filter/iir/interp.rs:51"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.get_interpolation(), 2)
+
+
+def test_filter_iir_interp_l70():
+    """src/filter/iir/interp.rs:70"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    numerators = filter.numerator_coefs()
+    orig_ratio = coefficients[0][0] / coefficients[0][1]
+    new_ratio = numerators[0] / numerators[1]
+    _eq(orig_ratio, new_ratio)
+
+
+def test_filter_iir_interp_l94():
+    """src/filter/iir/interp.rs:94"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.Normal, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    denominators = filter.denominator_coefs()
+    orig_ratio = coefficients[1][0] / coefficients[1][1]
+    new_ratio = denominators[1] / denominators[0]
+    assert abs(orig_ratio - new_ratio) < 0.00001
+
+
+def test_filter_iir_interp_l118():
+    """src/filter/iir/interp.rs:118"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filters = filter.second_order_filters()
+    _eq(_len(filters), 1)
+
+
+def test_filter_iir_interp_l140():
+    """src/filter/iir/interp.rs:140"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    _eq(filter.iir_type(), IIRFilterType.SecondOrder)
+
+
+def test_filter_iir_interp_l170():
+    """src/filter/iir/interp.rs:170"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2)
+    output = filter.execute(1.0)
+    _eq(output, [0.05816769596076701, 0.119535296293297])
+
+
+def test_filter_iir_interp_l198():
+    """src/filter/iir/interp.rs:198"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    interpolation = 5
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, interpolation)
+    input = [1.0, 0.0, 1.0, 0.0, 1.0]
+    output = filter.execute_block(input)
+    _eq(_len(output), _len(input) * interpolation)
+
+
+def test_filter_iir_interp_l227():
+    """src/filter/iir/interp.rs:227"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2)
+    output = filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    freq_res = filter.frequency_response(0.0)
+    _eq(freq_res, complex(0.0, 0.0))
+
+
+def test_filter_iir_interp_l250():
+    """src/filter/iir/interp.rs:250"""
+    coefficients = iirdes.pll.active_lag(0.02, 1.0 / math.sqrt(2.0), 1000.0)
+    filter = InterpolatingIIRFilter.new(coefficients[0], coefficients[1], IIRFilterType.SecondOrder, 2)
+    output = filter.execute_block([1.0, 0.0, 1.0, 0.0, 1.0])
+    delay = filter.group_delay(0.0)
+    _eq(delay, 19.6774211296624)
+
+
+def test_dot_product_mod_l51():
+    """src/dot_product/mod.rs:51"""
+    coefs = [1.0, 2.0, 3.0, 4.0, 5.0]
+    dp = DotProduct.new(coefs, Direction.REVERSE)
+
+
+def test_dot_product_mod_l93():
+    """src/dot_product/mod.rs:93"""
+    coefs = [1.0, 2.0, 3.0, 4.0, 5.0]
+    dp = DotProduct.new(coefs, Direction.FORWARD)
+    ref_coefs = dp.coefficents()
+    _eq(coefs, ref_coefs)
+
+
+def test_dot_product_mod_l115():
+    """src/dot_product/mod.rs:115"""
+    coefs = [1.0, 2.0, 3.0, 4.0, 5.0]
+    dp = DotProduct.new(coefs, Direction.REVERSE)
+    _eq(_len(dp), 5)
+
+
+def test_dot_product_mod_l132():
+    """src/dot_product/mod.rs:132"""
+    coefs = [1.0, 2.0, 3.0, 4.0, 5.0]
+    dp = DotProduct.new(coefs, Direction.REVERSE)
+    _eq(dp.is_empty(), False)
+
+
+def test_dot_product_execute_l7():
+    """src/dot_product/execute.rs:7"""
+    coefs = [1.0, 2.0, 3.0, 4.0, 5.0]
+    dp = DotProduct.new(coefs, Direction.REVERSE)
+    mul = [1.0] * 5
+    exe = dp.execute(mul)
+    _eq(exe, 15.0)

@@ -117,7 +117,7 @@ def test_world2_gloo_full_gather_chunks():
 
 @pytest.mark.parametrize("shard", ["channel", "time"])
 @pytest.mark.parametrize("config,fault", [(2, ""), (4, ""), (2, "shift"), (4, "shift"), (3, ""), (3, "shift"),
-                                          (5, ""), (5, "shift")])
+                                          (3, "noexchange"), (5, ""), (5, "shift")])
 def test_bench_gpus2_dry_run_checks_gathered_output(config, fault, shard):
     """`bench.py --gpus 2 --dry-run` launches two ranks itself, runs the config's
     workload math per channel (the f64 restatement standing in for the device),
@@ -125,12 +125,16 @@ def test_bench_gpus2_dry_run_checks_gathered_output(config, fault, shard):
     path uses, and checks it with the same check_gathered: a rank whose output is one
     sample late must fail the check.  --shard time: one stream
     time-sharded, each rank's segment after its halo, checked inside and across the
-    segment boundaries (check_time_sharded)."""
+    segment boundaries (check_time_sharded); config 3 time-sharded joins its segments with
+    the one all_gather of boundary states (parallel.iir_exclusive_scan) -- without that
+    exchange (SDSP_DRYRUN_FAULT=noexchange) the check must fail."""
     import json
     import subprocess
     import sys
-    if config in (3, 5) and shard == "time":
-        pytest.skip("configs 3 and 5 shard by channel (stream) only")
+    if config == 5 and shard == "time":
+        pytest.skip("config 5 shards by stream only")
+    if fault == "noexchange" and shard != "time":
+        pytest.skip("the boundary-state exchange belongs to the IIR time shard")
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
     env["SDSP_DRYRUN_FAULT"] = fault
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run", "--config",
@@ -255,3 +259,86 @@ def test_bench_rejects_gpus_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.parametrize("case", ["butter8", "active_lag"])
+def test_iir_time_shard_exchange_reproduces_the_single_stream(case):
+    """SURVEY §8e IIR time shard on the f64 restatement: three segments of one stream, each
+    run from zero state; the exclusive scan of their final states (Phi = A^n) gives each
+    segment's true initial state, and adding its zero-input response reproduces the single
+    stream -- for the decaying butter(8) cascade and for the reference demo's active_lag PLL
+    filter, whose integrator state never decays (zero_input_length = the whole segment)"""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+    from solid_dsp_amd import parallel as P
+    if case == "butter8":
+        sos = np.array(json.load(open(os.path.join(REPO, "tests", "golden", "butter8_0p2_sos.json")))["sos"])
+        ff, fb = sos[:, :3].reshape(-1), sos[:, 3:].reshape(-1)
+    else:
+        ff, fb = O.active_lag(0.02, 1 / np.sqrt(2.0), 1000.0)
+    n, R = 6000, 3  # butter8: the zero-input response is below rounding after 4096 samples
+    x = O.synth(5, 0, 0, R * n).astype(np.float64)
+    full = O.iir(O.RR64, ff, fb, O.SECOND_ORDER).execute_block(x)
+    A, b, c, d = P.sos_state_space(ff, fb)
+    W = P.zero_input_length(A, c, n)
+    assert (W < n) == (case == "butter8")
+    ys, states = [], []
+    for r in range(R):
+        o = O.iir(O.RR64, ff, fb, O.SECOND_ORDER)
+        ys.append(o.execute_block(x[r * n:(r + 1) * n]))
+        states.append(o.sos_state())
+    inits = P.iir_exclusive_scan(states, P.state_transition(A, n))
+    got = []
+    for r in range(R):
+        g = O.iir(O.RR64, ff, fb, O.SECOND_ORDER)
+        g.sos_state(inits[r])
+        y = ys[r].copy()
+        y[:W] += g.execute_block(np.zeros(W))
+        got.append(y)
+    got = np.concatenate(got)
+    scale = np.abs(full).max()
+    # butter8: rounding only.  active_lag's states run ~1e6 x its output and A^n of its
+    # double pole at z = 1 grows with n, so the re-associated sum (any split of one stream)
+    # is ~1e-7 relative -- the conditioning the wave scan refuses such cascades for
+    tol = 1e-12 if case == "butter8" else 1e-6
+    assert np.abs(got - full).max() <= tol * scale, np.abs(got - full).max() / scale
+    # the state-space model is the recurrence: one step from a random state
+    rng = np.random.default_rng(1)
+    st = rng.standard_normal(2 * (len(ff) // 3))
+    o = O.iir(O.RR64, ff, fb, O.SECOND_ORDER)
+    o.sos_state(st)
+    y1 = o.execute_block(np.array([0.7]))[0]
+    assert np.allclose(o.sos_state(), A @ st + b * 0.7, rtol=1e-12, atol=1e-12)
+    assert np.isclose(y1, c @ st + d * 0.7, rtol=1e-12, atol=1e-12)
+    # without the exchange the segment boundaries are wrong
+    bad = np.concatenate(ys)
+    assert np.abs(bad - full).max() > 1e-6 * scale
+
+
+def test_world2_gloo_state_exchange():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pc = mp.spawn(_state_exchange_worker, args=(2, _free_port(), q), nprocs=2, join=False)
+    got = q.get(timeout=120)
+    while not pc.join(timeout=60):
+        pass
+    assert len(got) == 2
+    for r in range(2):
+        assert np.array_equal(got[r], np.arange(8) + 100.0 * r)
+
+
+def _state_exchange_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, REPO)
+        from solid_dsp_amd import parallel as P
+        got = P.exchange_states(np.arange(8) + 100.0 * rank)
+        if rank == 0:
+            q.put([np.asarray(g) for g in got])
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

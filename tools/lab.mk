@@ -19,9 +19,12 @@ PRODUCT_OBJS = $(filter-out $(REPLACED),$(wildcard $(OBJ)/*.o))
 
 all: $(OUT)
 
-tools/_build/lab/%.o: tools/lab/%.hip $(CSRC)/*.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
+tools/_build/lab/%.o: tools/lab/%.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
 	@mkdir -p tools/_build/lab
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# each lab TU compiles its product source
+$(foreach m,$(LAB_MAP),$(eval tools/_build/lab/$(word 1,$(subst :, ,$(m))).o: $(CSRC)/$(word 2,$(subst :, ,$(m))).hip))
 
 tools/_build/lab/iir_lab.o: HIPFLAGS += -fno-slp-vectorize
 

@@ -1,8 +1,18 @@
 """Port the reference's doctests of the hot path (the files of SURVEY §8a that the
-shim replaces) into rust/solid-sdsp/tests/reference_doctests.rs: every ```-fenced
-example of a doc comment becomes one #[test] against the `solid` shim crate, body
-unchanged.  Run in this container (it reads /root/reference);
-the generated file is committed.
+shim replaces):
+
+ * rust/solid-sdsp/tests/reference_doctests.rs: every ```-fenced example of a doc
+   comment becomes one #[test] against the `solid` shim crate, body unchanged
+   (needs cargo, absent from this image);
+ * tests/test_gpu_reference_doctests.py: the same examples
+   translated statement by statement to the Python mirror of the same C ABI
+   (solid_dsp_amd), so each doctest's calls and asserted literals run on the
+   MI355X under `pytest -m gpu`.  The translation covers the Rust subset these
+   doctests use (let / tuple bindings, turbofish constructors, unwrap, Complex::new,
+   vec!, assert_eq! / assert!, match Ok(..), tuple fields, casts); a statement
+   outside it raises, so every doctest is either translated or reported.
+
+Run in this container (it reads /root/reference); the generated files are committed.
 
     python tools/port_doctests.py
 """
@@ -12,6 +22,7 @@ import re
 REF = "/root/reference/src"
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "rust", "solid-sdsp", "tests", "reference_doctests.rs")
+OUT_PY = os.path.join(REPO, "tests", "test_gpu_reference_doctests.py")
 FILES = ["filter/fir/mod.rs", "filter/fir/decim.rs", "filter/fir/interp.rs", "filter/fir/pfb.rs",
          "filter/iir/mod.rs", "filter/iir/sos.rs", "filter/iir/decim.rs", "filter/iir/interp.rs",
          "dot_product/mod.rs", "dot_product/execute.rs"]
@@ -39,6 +50,152 @@ def doctests(path):
     return out
 
 
+# ---------------------------------------------------------------- Rust subset -> Python
+_DT = {"f64": "np.float64", "f32": "np.float32", "Complex<f64>": "np.complex128", "Complex<f32>": "np.complex64"}
+
+
+def _statements(body):
+    """split a doctest body into top-level statements (';' outside brackets / braces);
+    `use` lines dropped"""
+    text = "\n".join(l for l in body if not l.strip().startswith("use "))
+    out, depth, cur = [], 0, ""
+    for ch in text:
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+        if ch == ";" and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return [" ".join(st.split()) for st in out if st.strip()]
+
+
+def _close_paren(s, i):
+    """index of the ')' matching the '(' at s[i]"""
+    depth = 0
+    for j in range(i, len(s)):
+        depth += s[j] == "("
+        depth -= s[j] == ")"
+        if depth == 0:
+            return j
+    raise ValueError("unbalanced: " + s)
+
+
+def _turbofish(s):
+    """Type::<Coef, In>::new(args) -> Type.new(args, coef_dtype=..., sample_dtype=...)"""
+    pat = re.compile(r"(\w+)::<(\w+(?:<\w+>)?), (\w+(?:<\w+>)?)>::new\(")
+    while True:
+        m = pat.search(s)
+        if not m:
+            return s
+        j = _close_paren(s, m.end() - 1)
+        kw = ", coef_dtype=%s, sample_dtype=%s" % (_DT[m.group(2)], _DT[m.group(3)])
+        s = s[:m.start()] + m.group(1) + ".new(" + s[m.end():j] + kw + s[j:]
+
+
+def _expr(e):
+    e = re.sub(r"match (.+?) \{ Ok\((\w+)\) => \2, _ => vec!\(\) \}", r"\1", e)
+    e = _turbofish(e)
+    e = e.replace(".unwrap()", "").replace(".to_vec()", "")
+    e = e.replace("either::Either::Right(", "(").replace("either::Either::Left(", "(")
+    e = re.sub(r"Filter::(\w+)\(&?(\w+), ", r"\2.\1(", e)
+    e = re.sub(r"(?:solid::filter::)?iirdes::pll::", "iirdes.pll.", e)
+    e = re.sub(r"(?:solid::filter::)?firdes::", "firdes.", e)
+    e = e.replace("Complex::new(", "complex(")
+    e = re.sub(r"vec!\[([^\[\];]*); (\w+)\]", r"[\1] * \2", e)
+    e = e.replace("vec![", "[").replace("vec!()", "[]")
+    e = re.sub(r"\((\d+)f64\)\.sqrt\(\)", r"math.sqrt(\1.0)", e)
+    e = re.sub(r"\b(\d+)f64\b", r"\1.0", e)
+    e = re.sub(r"\b(\w+)::new\(", r"\1.new(", e)
+    e = re.sub(r"\b(\w+)::(\w+)", r"\1.\2", e)
+    e = re.sub(r"(^|[(,\s])&(?=[\w\[(])", r"\1", e)
+    e = re.sub(r"(^|[(,\s])\*(?=\w)", r"\1", e)
+    e = re.sub(r"(?<=[A-Za-z_)\]])\.(\d+)\b", r"[\1]", e)
+    e = re.sub(r"\(([^()]*)\) as usize", r"int(\1)", e)
+    e = re.sub(r"\(([^()]*)\)\.abs\(\)", r"abs(\1)", e)
+    e = re.sub(r"([\w.]+)\.re\.round\(\)", r"_round(\1.real)", e)
+    e = re.sub(r"\.re\b", ".real", e)
+    e = re.sub(r"\.im\b", ".imag", e)
+    e = re.sub(r"\b(\w+)\.len\(\)", r"_len(\1)", e)
+    e = re.sub(r"\bfalse\b", "False", e)
+    e = re.sub(r"\btrue\b", "True", e)
+    if "::" in e or "!" in e.replace("!=", "") or "&" in e:
+        raise ValueError("outside the translated subset: " + e)
+    return e
+
+
+def to_python(body):
+    out = []
+    for st in _statements(body):
+        m = re.match(r"let (?:mut )?\((\w+), (\w+)\) = (.+)$", st)
+        if m:
+            out.append("%s, %s = %s" % (m.group(1), m.group(2), _expr(m.group(3))))
+            continue
+        m = re.match(r"let (?:mut )?(\w+)(?:: [^=]+)? = (.+)$", st)
+        if m:
+            out.append("%s = %s" % (m.group(1), _expr(m.group(2))))
+            continue
+        m = re.match(r"assert_eq!\((.+)\)$", st)
+        if m:
+            out.append("_eq(%s)" % _expr(m.group(1)))
+            continue
+        m = re.match(r"assert!\((.+)\)$", st)
+        if m:
+            out.append("assert %s" % _expr(m.group(1)))
+            continue
+        out.append(_expr(st))
+    return out
+
+
+PY_HEAD = '''"""The reference's doctests of the hot path (juliantos/solid-dsp src/filter/{fir,iir}/*.rs,
+src/dot_product/*.rs), translated statement by statement by tools/port_doctests.py to the
+Python mirror of the C ABI (solid_dsp_amd) and run on the MI355X: every call goes through
+libsdsp.so, and each asserted literal is the reference's, compared exactly as Rust's
+assert_eq! compares (f64 / Complex<f64> equality).  Generated -- edit the porter, not this file."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+sd = pytest.importorskip("solid_dsp_amd")
+from solid_dsp_amd import (FIRFilter, DecimatingFIRFilter, InterpolatingFIRFilter, PolyPhaseFilterBank,  # noqa
+                           IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter, InterpolatingIIRFilter,
+                           DotProduct, Direction)
+from solid_dsp_amd.filter import firdes, iirdes  # noqa: E402
+from solid_dsp_amd.filter.firdes import *  # noqa: E402,F401,F403
+
+
+def _plain(v):
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, (list, tuple)):
+        return [_plain(u) for u in v]
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def _eq(a, b):
+    """assert_eq!: exact equality, element by element for sequences"""
+    pa, pb = _plain(a), _plain(b)
+    assert pa == pb, (pa, pb)
+
+
+def _len(x):
+    return x.len() if hasattr(x, "len") and callable(x.len) else len(x)
+
+
+def _round(v):  # f64::round: half away from zero
+    return math.floor(v + 0.5) if v >= 0 else -math.floor(-v + 0.5)
+'''
+
+
 def main():
     parts = ["// Generated by tools/port_doctests.py from the reference's doc comments (juliantos/solid-dsp",
              "// src/filter/{fir,iir}/*.rs, src/dot_product/*.rs): each doctest, body unchanged, as an",
@@ -60,6 +217,18 @@ def main():
     with open(OUT, "w") as fh:
         fh.write("\n".join(parts))
     print("%d doctests -> %s" % (total, OUT))
+    py = [PY_HEAD]
+    for f in FILES:
+        tag = f.replace("/", "_").replace(".rs", "")
+        for start, body in doctests(os.path.join(REF, f)):
+            py.append("")
+            py.append("def test_%s_l%d():" % (tag, start))
+            py.append('    """src/%s:%d"""' % (f, start))
+            py += ["    " + ln for ln in to_python(body)] or ["    pass"]
+            py.append("")
+    with open(OUT_PY, "w") as fh:
+        fh.write("\n".join(py))
+    print("%d doctests -> %s" % (total, OUT_PY))
 
 
 if __name__ == "__main__":
