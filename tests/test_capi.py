@@ -81,3 +81,41 @@ def test_rust_shim_binds_only_declared_symbols():
     rs = open(os.path.join(repo, "rust", "solid-sdsp", "src", "sys.rs")).read()
     bound = set(re.findall(r"pub fn (sdsp_\w+)\s*\(", rs))
     assert bound and not (bound - declared), sorted(bound - declared)
+
+
+# ---------------------------------------------------------------- channeliser asm-load proof
+def _chk():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("check_chan_asm", os.path.join(REPO, "tools", "check_chan_asm.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_chan_asm_loads_are_covered_in_the_built_object():
+    """the untracked prefetch of chan1024_kernel<K, 1024, true, 8> is read only after
+    a provably covering vmcnt wait on every path, with no scratch (tools/check_chan_asm.py,
+    also run by the Makefile)"""
+    obj = os.path.join(REPO, "solid_dsp_amd", "_build", "obj", "kern_chan1024.o")
+    if not os.path.exists(obj):
+        pytest.skip("libsdsp not built")
+    assert _chk().main(obj) == 0
+
+
+def test_chan_asm_checker_flags_unsafe_code():
+    m = _chk()
+    ld = [(0x10 + 8 * i, "buffer_load_dwordx2", f" v[{2 * i}:{2 * i + 1}], v40, s[0:3], 0 offen", None)
+          for i in range(8)]
+    pro = ld + [(0x60, "s_waitcnt", " vmcnt(0)", None)]  # a prologue group, waited at once
+    base = 0x100
+    loop = [(base + 8 * i, mn, ops, None) for i, (mn, ops) in enumerate(
+        [("buffer_load_dwordx2", f" v[{2 * i}:{2 * i + 1}], v40, s[0:3], 0 offen") for i in range(8)]
+        + [("buffer_store_dwordx2", " v[20:21], v41, s[4:7], 0 offen nt")] * 16
+        + [("s_waitcnt", " vmcnt(16)"), ("v_mov_b64_e32", " v[30:31], v[2:3]"), ("s_endpgm", "")])]
+    assert m.check_kernel(pro + loop) == []
+    early = loop[:8] + loop[8:8 + 15] + loop[24:]  # one store short: vmcnt(16) no longer covers
+    assert m.check_kernel(pro + early)
+    use = loop[:8] + [(0x200, "v_add_f32_e32", " v50, v3, v4", None)] + loop[8:]
+    assert m.check_kernel(pro + use)
+    spill = pro + loop[:-1] + [(0x300, "scratch_store_dword", " off, v1, s0", None), loop[-1]]
+    assert m.check_kernel(spill)
