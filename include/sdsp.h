@@ -133,8 +133,10 @@ SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
  * (retired keys of earlier builds are rejected with SDSP_E_INVALID_ARGUMENT). */
 typedef enum {
     SDSP_TUNE_DECIM_SEG = 6,     /* FMA decimator: outputs per lane group (0 = automatic) */
-    SDSP_TUNE_IIR_WAVE_SCAN = 7, /* IIR scan kernel: 0 = block scan, 1 (default) = wave scan with 256-byte chunks,
-                                    2 = 128-byte chunks, 3/4 = paired 128/64-byte chunks (real f32) */
+    SDSP_TUNE_IIR_WAVE_SCAN = 7, /* IIR scan kernel: 0 = block scan, 1 = wave scan with 256-byte chunks (default
+                                    for complex and f64 samples), 2 = 128-byte chunks (default for real f32),
+                                    3/4 = paired 128/64-byte chunks (real f32), 5 = 256-byte chunks rerun
+                                    instead of corrected, 6 = 128-byte chunks without the register prefetch */
     SDSP_TUNE_CHAN_STREAMING = 8, /* channeliser: streaming M=1024 kernel where it applies: 3 = 1024-thread
                                      workgroups, sixteen frames per round, the next round's samples
                                      requested before this round's stores; 1 = the same without; 2 / 4 =

@@ -82,7 +82,9 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // (never part of libsdsp.so).  Bits: 1 block barriers at the wave-local phase
 // boundaries; 2 no HBM traffic (ablation: outputs dropped); 4 HBM traffic only
 // (ablation: no transform); 128 plain (not nontemporal) stores; 256 input rows
-// loaded last to first; 512 output rows stored last to first.
+// loaded last to first; 512 output rows stored last to first; 1024 each XCD walks the
+// even segments of its eighth, then the odd ones (a segment's halo row is then read
+// long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss).
 template <int ABL>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -199,7 +201,9 @@ fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const
                   f2* __restrict__ y, long long n, long long lo, long long hi, long long q, int h2) {
     __shared__ __attribute__((aligned(16))) f2 img[16 * kRow];
     const int xc = blockIdx.x & 7;
-    const long long seg = lo + (long long)xc * q + (blockIdx.x >> 3);
+    long long j = blockIdx.x >> 3;
+    if constexpr ((ABL & 1024) != 0) j = j < (q + 1) / 2 ? 2 * j : 2 * (j - (q + 1) / 2) + 1;
+    const long long seg = lo + (long long)xc * q + j;
     const long long xe = lo + (long long)(xc + 1) * q;
     if (seg >= (xe < hi ? xe : hi)) return;  // uniform over the workgroup
     const int V = 4096 - 256 * h2;

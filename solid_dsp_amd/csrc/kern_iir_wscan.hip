@@ -31,9 +31,6 @@
 #include "sdsp_device.hpp"
 #include "sdsp_kernels.hpp"
 
-#include <map>
-#include <mutex>
-#include <tuple>
 #include <type_traits>
 
 namespace sdsp {
@@ -161,14 +158,7 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // slab so that 64 consecutive outputs leave per store instruction).
 // FORM: 0 correction by the state response, next tile prefetched into registers; 1 a
 // rerun from the true state instead of the correction; 2 the correction without the
-// register prefetch (fewer registers: more waves per SIMD hide the tile loads instead);
-// 3 independent tiles in time-major order (warm-up scans only, no rate change): every tile
-// starts from zero state with its own wc warm-up chunks (the previous tile's last chunks,
-// outputs dropped) and covers 64 - wc chunks of output, so the tiles need no carry from one
-// another and a persistent grid walks them XCD by XCD in time-major order -- at step t
-// the waves of an XCD's resident blocks hold neighbouring tiles (one narrow streaming
-// front per XCD) instead of each wave streaming its own segment.  nwaves = tiles of the
-// call; tpw = steps per wave.
+// register prefetch (fewer registers: more waves per SIMD hide the tile loads instead)
 // LAB selects compile-time variants for in-process A/B runs (tools/lab/iir_lab.hip; the product
 // kernels are LAB = 0): ablations 1 no zero-state run, 2 no scan, 4 no correction, 8 no HBM
 // loads, 16 no HBM stores; variants 32 plain (not nontemporal) loads, 64 plain stores
@@ -181,7 +171,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                  long long nwaves) {
     constexpr int D = ND ? ND : 2 * S;
     constexpr int B = ws_chunk<I, CB>::B;
-    constexpr bool RERUN = FORM == 1, PF = FORM != 2, TM = FORM == 3;
+    constexpr bool RERUN = FORM == 1, PF = FORM != 2;
     constexpr int E = 16 / (int)sizeof(I);  // samples per 16-byte vector
     constexpr int kRowBytes = WsGeom<CB>::kRowBytes, kVecPerRow = WsGeom<CB>::kVecPerRow;
     constexpr int kSlabBytes = WsGeom<CB>::kSlabBytes;
@@ -215,19 +205,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     const long long segc = (long long)tpw * 64 - wc;  // chunks per segment
     const long long c_lo = gw * segc;                 // first chunk of the segment
     const long long k_lo = c_lo * B;
-    // TM: tile g covers output chunks [g (64 - wc), (g + 1) (64 - wc)); XCD x owns tiles
-    // [x Q, (x + 1) Q) and its blocks take them in time-major order
-    const long long tm_q = (nwaves + 7) / 8, tm_lo = (long long)(blockIdx.x & 7) * tm_q;
-    const long long tm_hi = tm_lo + tm_q < nwaves ? tm_lo + tm_q : nwaves;
-    auto tm_tile = [&](int t) {
-        return tm_lo + ((long long)t * (gridDim.x / 8) + (blockIdx.x >> 3)) * kWsWaves + wave;
-    };
-    auto tm_k0 = [&](long long g) { return (g * (64 - wc) - wc) * B; };
-    if constexpr (TM) {
-        if (tm_tile(0) >= tm_hi) return;
-    } else {
-        if (k_lo >= nd) return;
-    }
+    if (k_lo >= nd) return;
 
     // carry entering the wave's first tile: zero (warm-up lanes settle it, wave 0 injects
     // st_in), or the exact carry of the aggregate pass + carry scan (cin)
@@ -241,7 +219,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     auto interior_at = [&](long long k0) { return vec_ok && Mi == 1 && k0 >= 0 && k0 + 64LL * B <= nd; };
     v4u pre[kVecPerRow];
     if constexpr (PF) {
-        const long long k0 = TM ? tm_k0(tm_tile(0)) : (c_lo - wc) * B;
+        const long long k0 = (c_lo - wc) * B;
         if (interior_at(k0)) {
 #pragma unroll
             for (int j = 0; j < kVecPerRow; ++j)
@@ -252,21 +230,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     }
 
     for (int t = 0; t < tpw; ++t) {
-        long long k0, klo;  // first sample of the tile, first sample whose output the tile stores
-        bool first_tile;    // the call's first samples: the exact carried state enters here
-        if constexpr (TM) {
-            const long long g = tm_tile(t);
-            if (g >= tm_hi) break;
-            k0 = tm_k0(g);
-            klo = k0 + (long long)wc * B;
-            first_tile = g == 0;
-#pragma unroll
-            for (int d = 0; d < D; ++d) carry[d] = zero_v<I>();
-        } else {
-            k0 = (c_lo - wc + (long long)t * 64) * B;
-            klo = k_lo;
-            first_tile = gw == 0 && t == 0;
-        }
+        const long long k0 = (c_lo - wc + (long long)t * 64) * B;  // first sample of the tile
         if (k0 >= nd) break;
 
         // 1. stage the tile: vector v of the tile -> row v / kVecPerRow, slot v % kVecPerRow
@@ -295,8 +259,8 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             }
         }
         if constexpr (PF) {  // prefetch the next tile (whatever path this one took)
-            const long long kn = TM ? tm_k0(tm_tile(t + 1)) : k0 + 64LL * B;
-            if (t + 1 < tpw && (!TM || tm_tile(t + 1) < tm_hi) && interior_at(kn)) {
+            const long long kn = k0 + 64LL * B;
+            if (t + 1 < tpw && interior_at(kn)) {
 #pragma unroll
                 for (int j = 0; j < kVecPerRow; ++j)
                     pre[j] = (lab & 8)    ? v4u{(unsigned)lane, (unsigned)t, 0u, (unsigned)j}
@@ -321,7 +285,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 if constexpr (!RERUN) *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
             }
         }
-        if (!cin && !agg && first_tile && lane == wc - 1) {  // the call's exact carried state enters here
+        if (!cin && !agg && gw == 0 && t == 0 && lane == wc - 1) {  // the call's exact carried state enters here
 #pragma unroll
             for (int d = 0; d < D; ++d) s[d] = st_in[d];
         }
@@ -394,7 +358,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 
         // exact final state: the lane of this segment holding sample nd-1 reruns its chunk
         const long long kc = k0 + (long long)lane * B;
-        if (kc >= klo && kc <= nd - 1 && nd - 1 < kc + B) {
+        if (kc >= k_lo && kc <= nd - 1 && nd - 1 < kc + B) {
             I st[D];
 #pragma unroll
             for (int d = 0; d < D; ++d) st[d] = init[d];
@@ -417,17 +381,6 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                                                        (pos % E) * (int)sizeof(I));
                 }
             }
-        } else if (TM && interior) {
-            // the tile's own outputs: rows >= wc.  A buffer descriptor over them drops the warm-up
-            // rows' stores (their offsets wrap past num_records), with no branch around the stores
-            const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + klo), (short)0, (64 - wc) * CB, 0x00020000);
-#pragma unroll
-            for (int j = 0; j < kVecPerRow; ++j) {
-                const int v = lane + 64 * j;
-                const v4u val = *reinterpret_cast<const v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16);
-                if ((lab & 16) && val.x != 0x7fc01234u) continue;  // ablation: stores dropped
-                __builtin_amdgcn_raw_buffer_store_b128(val, ry, (unsigned)(v * 16 - wc * CB), 0, (lab & 64) ? 0 : 2);
-            }
         } else if (interior && k0 >= k_lo) {
 #pragma unroll
             for (int j = 0; j < kVecPerRow; ++j) {
@@ -447,7 +400,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 __builtin_memcpy(tmp, &val, 16);
 #pragma unroll
                 for (int e = 0; e < E; ++e)
-                    if (kv + e >= klo && kv + e < nd) y[kv + e] = tmp[e];
+                    if (kv + e >= k_lo && kv + e < nd) y[kv + e] = tmp[e];
             }
         }
         wave_sync();
@@ -836,26 +789,6 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-// resident blocks of a wave-scan kernel on the current device (CU count x occupancy at `lds`
-// bytes, rounded down to whole XCDs), looked up once per (device, kernel, LDS size)
-long long wscan_resident_blocks(const void* kern, size_t lds) {
-    static std::mutex mu;
-    static std::map<std::tuple<int, const void*, size_t>, long long> cache;
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    const auto key = std::make_tuple(dev, kern, lds);
-    std::lock_guard<std::mutex> g(mu);
-    const auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int cus = 256, per_cu = 0;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kWsThreads, lds);
-    long long r = (long long)(per_cu > 0 ? per_cu : 1) * cus / 8 * 8;
-    if (r < 8) r = 8;
-    cache.emplace(key, r);
-    return r;
-}
-
 template <int CB> int wscan_tpw(long long nch) {
     // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
     int tpw = (int)(nch / (64LL * 4096));
@@ -870,21 +803,6 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st, int tpw_force = 0) {
     constexpr int D = ND ? ND : 2 * S;
     const long long nd = (long long)a.n * a.Mi;  // domain samples
     const long long nch = (nd + B - 1) / B;
-    if constexpr (FORM == 3) {  // independent tiles, persistent time-major grid
-        if (a.wc <= 0 || a.wc >= 64 || a.Mi != 1 || a.Md != 1) return hipErrorInvalidValue;
-        const long long own = 64 - a.wc, ntiles = (nch + own - 1) / own;
-        const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * D * D);
-        auto kern = sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>;
-        const long long gx = wscan_resident_blocks((const void*)kern, lds) / 8;  // resident blocks per XCD
-        const long long steps = ((ntiles + 7) / 8 + gx * kWsWaves - 1) / (gx * kWsWaves);
-        const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
-                            (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
-        hipLaunchKernelGGL(kern, dim3((unsigned)(8 * gx), (unsigned)a.channels), dim3(kWsThreads), lds, st,
-                           (const I*)a.x, (I*)a.y, (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in,
-                           (I*)a.st_out, nd, a.wc, (int)steps, vec_ok, 1, 1, 0LL, nd, (const I*)nullptr, (I*)nullptr,
-                           ntiles);
-        return hipGetLastError();
-    }
     int tpw = wscan_tpw<CB>(nch);
     if (a.wc > 0 && tpw_force > 0) tpw = tpw_force;
     const long long segc = (long long)tpw * 64 - a.wc;

@@ -330,12 +330,15 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
 // one-block carry kernel, Phi^R (R = ceil(W / 256), by repeated squaring in the Coef
 // type) and 256 chained applications of it: the carried state is multiplied by
 // powers of Phi up to Phi^W.  The plan-time probe covers chunk carries over 2^14
-// samples only, so each call also bounds the powers it will use: ||Phi^(2^j)||_inf <=
-// 1e6 for every 2^j < 2 W (checked in f64, once per tpw, cached as the largest W
-// admitted).  A marginally stable system whose powers grow (a double pole at z = 1:
-// ||A^m|| ~ m) is admitted for short calls and runs the reference-order recurrence
-// for long ones; bounded powers (a single pole at z = 1, poles on the unit circle)
-// admit every length.
+// samples only, so each call also bounds the powers it will use: every
+// power Phi^m with m < 2^(j+1) is a product of a subset of the repeated squares
+// Phi^(2^0) .. Phi^(2^j), so ||Phi^m||_inf <= prod_{i<=j} max(1, ||Phi^(2^i)||_inf); a call
+// of W waves is admitted while that product stays <= 1e6 for 2^(j+1) > W (computed in
+// f64, once per tpw, cached as the largest W admitted).  This is a bound, not a
+// heuristic, on the growth of the carried state; a marginally stable system whose
+// powers grow (a double pole at z = 1: ||A^m|| ~ m) is admitted for short calls and
+// runs the reference-order recurrence for long ones, and systems with bounded powers
+// (a single pole at z = 1, poles on the unit circle) admit long calls.
 bool exact_carry_bounded(const sdsp_iir* h, Group& g, int wv, size_t waves, int tpw) {
     if (tpw < 1 || tpw > 8) return false;
     long long& wmax = g.ws[wv].phi_wmax[tpw];
@@ -343,10 +346,13 @@ bool exact_carry_bounded(const sdsp_iir* h, Group& g, int wv, size_t waves, int 
         const int D = group_dim(h, g), B = iir_wscan_chunk(h->dtype, wv);
         Mat P = matpow(matpow(sys_A(h, g), B, D), 64LL * tpw, D);
         wmax = 0;
+        double bound = 1.0;  // >= ||Phi^m||_inf for every m < 2^(j+1)
         for (int j = 0; j < 48; ++j) {
             const double nrm = norm_inf(P, D);
-            if (!std::isfinite(nrm) || nrm > 1e6) break;
-            wmax = (2LL << j) - 1;  // every power up to 2^(j+1) - 1 is a product of checked squares' neighbours
+            if (!std::isfinite(nrm)) break;
+            bound *= nrm > 1.0 ? nrm : 1.0;
+            if (bound > 1e6) break;
+            wmax = (2LL << j) - 1;  // powers up to 2^(j+1) - 1: products of Phi^(2^0) .. Phi^(2^j)
             P = matmul(P, P, D);
         }
     }

@@ -207,6 +207,7 @@ static int acorr_host(sdsp_acorr* h, const void* in, size_t n, void* out) {
     if (!h || (n && !in)) return SDSP_E_INVALID_ARGUMENT;
     if (n == 0) return SDSP_OK;
     Guard g(h->device);
+    R_TRY(h->fence.wait(), "wait for queued work");  // host slices: the last block first, on the host
     const size_t bytes = h->channels * n * cbytes(h->prec);
     R_TRY(h->stage_in.ensure(bytes), "stage in");
     R_TRY(hipMemcpyAsync(h->stage_in.p, in, bytes, hipMemcpyHostToDevice, h->stream), "H2D");
@@ -235,7 +236,7 @@ int sdsp_acorr_execute(sdsp_acorr* h, void* out) {
     Guard g(h->device);
     const size_t bytes = h->channels * cbytes(h->prec);
     R_TRY(h->stage_out.ensure(bytes), "stage out");
-    R_TRY(h->fence.order_before(h->stream), "order after queued work");
+    R_TRY(h->fence.wait(), "wait for queued work");  // host-side op: wait for the last block on the host
     R_TRY(launch_acorr_current(h->prec, h->hist[h->cur].p, h->stage_out.p, (int)h->W, (int)h->d, h->K(), h->channels,
                                h->stream),
           "acorr execute");
@@ -247,7 +248,7 @@ int sdsp_acorr_execute(sdsp_acorr* h, void* out) {
 int sdsp_acorr_get_energy(sdsp_acorr* h, double* energy) {
     if (!h || !energy) return SDSP_E_INVALID_ARGUMENT;
     Guard g(h->device);
-    R_TRY(h->fence.order_before(h->stream), "order after queued work");
+    R_TRY(h->fence.wait(), "wait for queued work");  // host-side op: wait for the last block on the host
     R_TRY(hipMemcpyAsync(energy, h->energy.p, h->channels * 8, hipMemcpyDeviceToHost, h->stream), "D2H");
     R_TRY(hipStreamSynchronize(h->stream), "sync");
     return SDSP_OK;

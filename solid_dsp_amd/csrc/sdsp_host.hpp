@@ -150,11 +150,16 @@ struct StreamFence {
         return hipSuccess;
     }
     // order work about to be queued on `s` after the pending marker (nothing to do on the
-    // marker's own stream: stream order)
+    // marker's own stream: stream order).  A marker on, or a wait from, the legacy null
+    // stream is waited for on the host instead: a device-side wait across it crashed the
+    // host side of the runtime in a round-4 GPU run (AutoCorrelator block on the legacy
+    // stream, then get_energy on the handle's stream)
     hipError_t order_before(hipStream_t s) {
         if (!pending || s == stream) return hipSuccess;
+        if (legacy(s) || legacy(stream)) return wait();
         return hipStreamWaitEvent(s, ev[cur], 0);
     }
+    static bool legacy(hipStream_t s) { return s == nullptr || s == hipStreamLegacy; }
     hipError_t wait() {
         if (!pending) return hipSuccess;
         pending = false;

@@ -29,7 +29,7 @@ $(foreach m,$(LAB_MAP),$(eval tools/_build/lab/$(word 1,$(subst :, ,$(m))).o: $(
 tools/_build/lab/iir_lab.o: HIPFLAGS += -fno-slp-vectorize
 
 $(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_TUS)) $(PRODUCT_OBJS)
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@ $^
+	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@.tmp $^ && mv -f $@.tmp $@
 
 # round-3 archive: the slot / pair / trio / quad / queue kernels (sdsp_lab_set_ols_variant
 # variants >= 256 of that round)

@@ -3,8 +3,7 @@
 // a launcher that runs sos_wscan_kernel<..., LAB> on real-f32 4-section warm-up
 // scans (the cfg3 shape) for the ablation set by sdsp_lab_set_iir_ablation
 // (tools/iir_ab.py).  LAB bits are documented at sos_wscan_kernel; bits 8-11 of
-// the ablation value force the tiles per wave, bit 12 selects FORM 3 (independent
-// tiles in time-major order).  tools/lab.mk links it in place of
+// the ablation value force the tiles per wave.  tools/lab.mk links it in place of
 // the product object.
 #define launch_iir_wscan launch_iir_wscan_product
 #include "kern_iir_wscan.hip"
@@ -14,12 +13,8 @@ namespace sdsp {
 
 static int g_iir_lab = 0;
 
-// bit 4096 of the ablation value: FORM 3 (independent tiles, time-major) instead of FORM 0
-static bool g_iir_tm = false;
-
 template <int CB, int LAB>
 static hipError_t lab_cfg3(const IirArgs& a, hipStream_t st, int tpw) {
-    if (g_iir_tm) return launch_wscan_t<float, float, 4, CB, 3, 0, LAB>(a, st, tpw);
     return launch_wscan_t<float, float, 4, CB, 0, 0, LAB>(a, st, tpw);
 }
 
@@ -41,8 +36,7 @@ static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw)
 
 hipError_t launch_iir_wscan(int dtype, const IirArgs& a, hipStream_t st) {
     const int ab = g_iir_lab & 255, tpw = (g_iir_lab >> 8) & 15;
-    g_iir_tm = (g_iir_lab & 4096) != 0;
-    if ((ab || tpw || g_iir_tm) && dtype == 0 && a.sections == 4 && a.Mi == 1 && a.Md == 1 && a.wc > 0 && a.n > 0) {
+    if ((ab || tpw) && dtype == 0 && a.sections == 4 && a.Mi == 1 && a.Md == 1 && a.wc > 0 && a.n > 0) {
         if (a.ws_variant == 1) return lab_cfg3_ab<128>(a, st, ab, tpw);
         if (a.ws_variant == 0) return lab_cfg3_ab<256>(a, st, ab, tpw);
     }
