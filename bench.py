@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--shard", default="channel", choices=["channel", "time"],
                    help="configs 2 and 4: independent channels per rank (default), or one long stream "
                         "time-sharded (rank r filters inputs [r n, (r+1) n) after an (L-1)-input halo)")
+    p.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
+                   help="kernel-variant knob on the workload's handle, e.g. FFT_WAVE1024=2 "
+                        "(SDSP_TUNE_<NAME>, include/sdsp.h); A/B runs only, the default line uses none")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU-only rehearsal of the rank launch, timing and gather over gloo (no GPU)")
     return p.parse_args()
@@ -1182,6 +1185,9 @@ def main():
 
     stream = torch.cuda.current_stream()
     w = WORKLOADS[args.config](args, rank, dev, torch, sd)
+    for kv in args.tune:
+        name, val = kv.split("=")
+        w.f.set_tuning(getattr(sd._lib, "TUNE_" + name.upper()), int(val))
     torch.cuda.synchronize()
     # achievable copy bandwidth of this box, measured before the warm-up: it also
     # brings the device out of its idle clocks (~0.3 s of streaming) so the
@@ -1259,7 +1265,7 @@ def main():
                      "synthetic SplitMix64 stream (seed 20250226, one channel; rank r generates its segment and halo), "
                      "device generated"),
             "config": {"workload": w.workload, "samples_per_step_per_gpu": w.samples_per_step,
-                       "kernel": w.kernel,
+                       "kernel": w.kernel, **({"tuning": args.tune} if args.tune else {}),
                        "parallelism": getattr(w, "parallelism", None) or f"channels sharded, independent per GPU x {world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -84,7 +84,9 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // (ablation: no transform); 128 plain (not nontemporal) stores; 256 input rows
 // loaded last to first; 512 output rows stored last to first; 1024 each XCD walks the
 // even segments of its eighth, then the odd ones (a segment's halo row is then read
-// long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss).
+// long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss);
+// ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
+// twiddle-base loads (wrong results, timing only).
 template <int ABL>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -112,12 +114,16 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         return;
     }
     // twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build)
-    const float4 b0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 0, 0));
-    const float4 b1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 4096, 0));
-    const float4 b2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * t, 8192, 0));
-    const float4 e0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12288, 0));
-    const float4 e1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12544, 0));
-    const float4 e2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lo4, 12800, 0));
+    auto tab = [&](int lane, int off) {
+        if constexpr ((ABL & 4096) != 0) {
+            const float u = 1e-3f * (float)lane + 1e-6f * (float)off;
+            return float4{u, 0.5f - u, 0.25f + u, 1.0f - u};
+        } else {
+            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lane, off, 0));
+        }
+    };
+    const float4 b0 = tab(t, 0), b1 = tab(t, 4096), b2 = tab(t, 8192);
+    const float4 e0 = tab(lo4, 12288), e1 = tab(lo4, 12544), e2 = tab(lo4, 12800);
     f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
     f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
     const f2 Eb[3] = {f2{e0.x, e0.y}, f2{e0.z, e0.w}, f2{e1.x, e1.y}};
@@ -136,7 +142,10 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
     float4 hq[8];  // spectrum slice of lane (k0, k1) = t for P3, k-pair major
 #pragma unroll
-    for (int p = 0; p < 8; ++p) hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+    for (int p = 0; p < 8; ++p) {
+        if constexpr ((ABL & 2048) != 0) hq[p] = float4{1e-3f * (float)t, (float)p, 0.5f, 1e-4f * (float)t};
+        else hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+    }
     f2 w2[16];  // W256^(lo4 k), used by P2 (n0 = lo4) and P3 (k1 = lo4)
 #pragma unroll
     for (int k = 1; k < 16; ++k) w2[k] = tw_pair(Eb, Fa, k);

@@ -188,7 +188,8 @@ def test_agc_kernel_variants_agree(kernel):
         g.set_tuning(L.TUNE_AGC_KERNEL, 2)
 
 
-@pytest.mark.parametrize("knob", [(L.TUNE_FFT_WAVE1024, 16), (L.TUNE_FFT_WAVE1024, 1), (L.TUNE_FFT_WAVE1024, 8),
+@pytest.mark.parametrize("knob", [(L.TUNE_FFT_WAVE1024, 16), (L.TUNE_FFT_WAVE1024, 2), (L.TUNE_FFT_WAVE1024, 1),
+                                  (L.TUNE_FFT_WAVE1024, 8),
                                   (L.TUNE_FFT_WAVE1024, 0), (L.TUNE_FFT_GROUP, 1), (L.TUNE_FFT_GROUP, 8)])
 def test_fft_pass_kernel_variants_agree(knob):
     """2^20-point c32 four-step FFT on each pass kernel (SDSP_TUNE_FFT_WAVE1024 = 0 runs the

@@ -23,6 +23,9 @@ for s in ${STEPS:-pytest}; do
         chanab) run chanab 600 python -u tools/chan_ab.py ;;
         bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} ;;
         bench_cfg*) run "$s" 300 python -u bench.py --config "${s#bench_cfg}" --steps 20 --warmup 5 --no-cpu ;;
+        # tune8_<NAME>_<VALUE>: config 8 with one kernel-variant knob
+        tune8_*) t=${s#tune8_}; run "$s" 300 python -u bench.py --config 8 --steps 20 --warmup 5 --no-cpu \
+                     --tune "${t%_*}=${t##*_}" ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
