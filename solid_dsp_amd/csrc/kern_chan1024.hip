@@ -214,6 +214,8 @@ __device__ __forceinline__ void chan_dummy_stores(f2* yf) {
     for (int k = 0; k < 16; ++k)  // distinct offsets: identical stores would be merged into one
         __builtin_amdgcn_raw_buffer_store_b64(chan_u2{0u, 0u}, rz, 0, 8 * k, 2);
 }
+// AUX: the stores' cache policy (2 nontemporal; 16 write-through sc1, a lab variant)
+template <int AUX = 2>
 __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw& tw, int L, f2* __restrict__ yf,
                                              bool store) {
     using pk::kout;
@@ -263,7 +265,7 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
         pk::pdft4<false>(r[0], r[1], r[2], r[3]);
 #pragma unroll
         for (int k0 = 0; k0 < 4; ++k0)  // nontemporal (aux 2)
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(chan_u2, r[k0]), ry, (L + 64 * bk + 256 * k0) * 8, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(chan_u2, r[k0]), ry, (L + 64 * bk + 256 * k0) * 8, 0, AUX);
     }
 }
 
@@ -280,7 +282,8 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // many of stores) and transform the round's frames on waves 0..R-1.
 // LAB selects compile-time variants for in-process A/B runs (tools/lab/chan_lab.hip; the
 // product kernels are LAB = 0): 1 no FFT, 2 no loads, 4 no stores (ablations); 8 / 16 odd
-// workgroups start ~6.8 / ~3.4 us late; 32 plain stores; 64 nontemporal loads.
+// workgroups start ~6.8 / ~3.4 us late; 32 plain stores; 64 nontemporal loads; 128 write-through
+// (sc1) stores.
 template <int K, int T, bool PF, int R = T / 64, int LAB = 0>
 __global__ void __launch_bounds__(T, T == 1024 ? 4 : 2)  // 1024 lanes: 4 waves per SIMD, 128 VGPRs
 chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
@@ -502,7 +505,7 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
 #pragma unroll
                         for (int k = 0; k < 16; ++k) st_nt2<(LAB & 32) != 0>(ys + f * kM + L + 64 * k, sbuf[w * kM + L + 64 * k]);
                 } else {
-                    fft1024_chan(sbuf + w * kM, stw, L, ys + f * kM, f < m_end && !(lab & 4));
+                    fft1024_chan<(LAB & 128) ? 16 : 2>(sbuf + w * kM, stw, L, ys + f * kM, f < m_end && !(lab & 4));
                 }
                 if (PF) wait_round(false);
                 __syncthreads();

@@ -86,7 +86,7 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // even segments of its eighth, then the odd ones (a segment's halo row is then read
 // long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss);
 // ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
-// twiddle-base loads (wrong results, timing only).
+// twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores.
 template <int ABL>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -109,7 +109,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
             const int r = (ABL & 512) ? 15 - i : i;
             if (r >= h2)
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[r]), ry, 8 * t, 2048 * r,
-                                                      (ABL & 128) ? 0 : 2);
+                                                      (ABL & 8192) ? 16 : (ABL & 128) ? 0 : 2);
         }
         return;
     }
@@ -195,7 +195,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         return;
     }
     // nontemporal stores (3.14 -> 3.08 ms on cfg2, in-process A/B)
-    constexpr int kStAux = (ABL & 128) ? 0 : 2;
+    constexpr int kStAux = (ABL & 8192) ? 16 : (ABL & 128) ? 0 : 2;  // 16: write-through (sc1), lab
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int r = (ABL & 512) ? 15 - i : i;

@@ -21,6 +21,7 @@ for s in ${STEPS:-pytest}; do
         olsab) OLS_ROUNDS=${ROUNDS:-15} OLS_CASES=${OLS_CASES:-0,256,4,260} run olsab 600 python -u tools/ols_lab.py ;;
         iirab) IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirab 600 python -u tools/iir_ab.py ;;
         chanab) run chanab 600 python -u tools/chan_ab.py ;;
+        copyprobe) run copyprobe 300 tools/_build/copy_shape_probe ;;
         bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} ;;
         bench_cfg*) run "$s" 300 python -u bench.py --config "${s#bench_cfg}" --steps 20 --warmup 5 --no-cpu ;;
         # tune8_<NAME>_<VALUE>: config 8 with one kernel-variant knob

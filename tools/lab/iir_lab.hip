@@ -30,6 +30,8 @@ static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw)
         case 24: return lab_cfg3<CB, 24>(a, st, tpw);
         case 32: return lab_cfg3<CB, 32>(a, st, tpw);
         case 64: return lab_cfg3<CB, 64>(a, st, tpw);
+        case 128: return lab_cfg3<CB, 128>(a, st, tpw);
+        case 136: return lab_cfg3<CB, 136>(a, st, tpw);
         default: return lab_cfg3<CB, 0>(a, st, tpw);
     }
 }
