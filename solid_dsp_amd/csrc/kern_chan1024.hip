@@ -282,8 +282,8 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // many of stores) and transform the round's frames on waves 0..R-1.
 // LAB selects compile-time variants for in-process A/B runs (tools/lab/chan_lab.hip; the
 // product kernels are LAB = 0): 1 no FFT, 2 no loads, 4 no stores (ablations); 8 / 16 odd
-// workgroups start ~6.8 / ~3.4 us late; 32 plain stores; 64 nontemporal loads; 128 write-through
-// (sc1) stores.
+// workgroups start ~6.8 / ~3.4 us late; 32 plain stores; 64 nontemporal loads (16-byte and
+// guarded paths); 128 write-through (sc1) stores; 256 nontemporal round loads (the asm path).
 template <int K, int T, bool PF, int R = T / 64, int LAB = 0>
 __global__ void __launch_bounds__(T, T == 1024 ? 4 : 2)  // 1024 lanes: 4 waves per SIMD, 128 VGPRs
 chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
@@ -412,10 +412,16 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
                     typedef unsigned u4s __attribute__((ext_vector_type(4)));
                     const u4s rw = {(unsigned)a, (unsigned)(a >> 32) & 0xffffu, nrec, 0x00020000u};
                     f2 r;
-                    asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen"
-                                 : "=v"(r)
-                                 : "v"((unsigned)(f * kM + kM - 1 - t) * 8), "s"(rw)
-                                 : "memory");
+                    if constexpr ((LAB & 256) != 0)
+                        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt"
+                                     : "=v"(r)
+                                     : "v"((unsigned)(f * kM + kM - 1 - t) * 8), "s"(rw)
+                                     : "memory");
+                    else
+                        asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen"
+                                     : "=v"(r)
+                                     : "v"((unsigned)(f * kM + kM - 1 - t) * 8), "s"(rw)
+                                     : "memory");
                     nx[f][0] = r;
                 }
             }

@@ -86,7 +86,9 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // even segments of its eighth, then the odd ones (a segment's halo row is then read
 // long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss);
 // ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
-// twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores.
+// twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores; 16384
+// nontemporal input loads; 32768 two of the six twiddle bases loaded, the rest as their
+// products (results within rounding of the product kernel's).
 template <int ABL>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -101,9 +103,13 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     for (int i = 0; i < 16; ++i) {
         const int r = (ABL & 256) ? 15 - i : i;
         if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
-        else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+        else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, (ABL & 16384) ? 2 : 0));
     }
     if constexpr (ABL & 4) {
+        // every row's load in flight before the first store, as in the transform (without this
+        // the compiler sinks each load into its store's `r >= h2` branch: one round trip per row)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(v[r]));
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int r = (ABL & 512) ? 15 - i : i;
@@ -122,12 +128,26 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
             return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lane, off, 0));
         }
     };
-    const float4 b0 = tab(t, 0), b1 = tab(t, 4096), b2 = tab(t, 8192);
-    const float4 e0 = tab(lo4, 12288), e1 = tab(lo4, 12544), e2 = tab(lo4, 12800);
-    f2 Cb[3] = {f2{b0.x, b0.y}, f2{b0.z, b0.w}, f2{b1.x, b1.y}};
-    f2 Da[3] = {f2{b1.z, b1.w}, f2{b2.x, b2.y}, f2{b2.z, b2.w}};
-    const f2 Eb[3] = {f2{e0.x, e0.y}, f2{e0.z, e0.w}, f2{e1.x, e1.y}};
-    const f2 Fa[3] = {f2{e1.z, e1.w}, f2{e2.x, e2.y}, f2{e2.z, e2.w}};
+    f2 Cb[3], Da[3], Eb[3], Fa[3];
+    if constexpr ((ABL & 32768) != 0) {
+        // lab: the first power of each base from L2, the others as products (W^2 = W W, ...)
+        auto tab2 = [&](int lane, int off) {
+            return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rt, 16 * lane, off, 0));
+        };
+        const f2 c1 = tab2(t, 0), d1 = tab2(t, 4096 + 8), e1 = tab2(lo4, 12288), f1 = tab2(lo4, 12544 + 8);
+        const f2 c2 = pmul(c1, c1), d2 = pmul(d1, d1), e2 = pmul(e1, e1), f2_ = pmul(f1, f1);
+        Cb[0] = c1, Cb[1] = c2, Cb[2] = pmul(c2, c1);
+        Da[0] = d1, Da[1] = d2, Da[2] = pmul(d2, d1);
+        Eb[0] = e1, Eb[1] = e2, Eb[2] = pmul(e2, e1);
+        Fa[0] = f1, Fa[1] = f2_, Fa[2] = pmul(f2_, f1);
+    } else {
+        const float4 b0 = tab(t, 0), b1 = tab(t, 4096), b2 = tab(t, 8192);
+        const float4 e0 = tab(lo4, 12288), e1 = tab(lo4, 12544), e2 = tab(lo4, 12800);
+        Cb[0] = f2{b0.x, b0.y}, Cb[1] = f2{b0.z, b0.w}, Cb[2] = f2{b1.x, b1.y};
+        Da[0] = f2{b1.z, b1.w}, Da[1] = f2{b2.x, b2.y}, Da[2] = f2{b2.z, b2.w};
+        Eb[0] = f2{e0.x, e0.y}, Eb[1] = f2{e0.z, e0.w}, Eb[2] = f2{e1.x, e1.y};
+        Fa[0] = f2{e1.z, e1.w}, Fa[1] = f2{e2.x, e2.y}, Fa[2] = f2{e2.z, e2.w};
+    }
     f2* col = img + t + (t >> 4);  // (r, t) at col[r * kRow]
 
     // P1: DFT16 n2 -> k0, * W4096^(t k0) -> (k0, t)

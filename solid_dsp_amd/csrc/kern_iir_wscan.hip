@@ -20,7 +20,7 @@
 //   4. outputs are corrected instead of rerun:  y[i] = y0[i] + Cr[i] . I_l,
 //      Cr[i] = c A^i (the output response to the state, precomputed on the
 //      host in f64, read as wave-uniform scalar loads), then leave with
-//      coalesced nontemporal 16-byte stores.
+//      coalesced write-through (sc1) 16-byte stores.
 // A wave's first tile starts `wc` chunks before its segment: those lanes run
 // the preceding input as warm-up (outputs dropped), which makes the carried-in
 // state exact to ||A^(wc B)|| < 1e-9 (f32) / 1e-17 (f64), the criterion the
@@ -162,7 +162,7 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // LAB selects compile-time variants for in-process A/B runs (tools/lab/iir_lab.hip; the product
 // kernels are LAB = 0): ablations 1 no zero-state run, 2 no scan, 4 no correction, 8 no HBM
 // loads, 16 no HBM stores; variants 32 plain (not nontemporal) loads, 64 plain stores, 128
-// write-through (sc1) stores
+// nontemporal stores (the round-3 product; the product's interior stores are write-through)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -383,15 +383,17 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 }
             }
         } else if (interior && k0 >= k_lo) {
-            [[maybe_unused]] const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + k0), (short)0, 0x7fffffff, 0x00020000);
+            const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + k0), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
             for (int j = 0; j < kVecPerRow; ++j) {
                 const int v = lane + 64 * j;
                 const v4u val = *reinterpret_cast<const v4u*>(slab + (v / kVecPerRow) * kRowBytes + (v % kVecPerRow) * 16);
                 if ((lab & 16) && val.x != 0x7fc01234u) continue;  // ablation: stores dropped
-                if constexpr ((lab & 128) != 0) __builtin_amdgcn_raw_buffer_store_b128(val, ry, v * 16, 0, 16);  // sc1
-                else if (lab & 64) reinterpret_cast<v4u*>(y + k0)[v] = val;  // lab: plain store
-                else __builtin_nontemporal_store(val, reinterpret_cast<v4u*>(y + k0) + v);
+                // write-through (sc1) stores: cfg3 1.736 -> 1.707 ms against nontemporal ones (two
+                // boxes, in-process A/B, profiles/r04/lab/r04b_iirab.log, r04c_iirab.log)
+                if constexpr ((lab & 128) != 0) __builtin_nontemporal_store(val, reinterpret_cast<v4u*>(y + k0) + v);
+                else if constexpr ((lab & 64) != 0) reinterpret_cast<v4u*>(y + k0)[v] = val;  // lab: plain store
+                else __builtin_amdgcn_raw_buffer_store_b128(val, ry, v * 16, 0, 16);
             }
         } else {
             for (int j = 0; j < kVecPerRow; ++j) {

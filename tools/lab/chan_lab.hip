@@ -20,6 +20,8 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
         case 32: return try_launch_chan1024_t<32>(a, s, err);
         case 64: return try_launch_chan1024_t<64>(a, s, err);
         case 128: return try_launch_chan1024_t<128>(a, s, err);
+        case 256: return try_launch_chan1024_t<256>(a, s, err);
+        case 384: return try_launch_chan1024_t<384>(a, s, err);
         default: return try_launch_chan1024_t<0>(a, s, err);
     }
 }

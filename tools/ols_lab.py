@@ -5,7 +5,8 @@ sdsp_lab_set_ols_variant.  Shuffled order every round, median of rounds
 (guide §5.4 rule 24), after a clock-settling phase.
 
   OLS_CASES="0,4,4:18432,20::4" OLS_ROUNDS=15 python tools/ols_lab.py
-A case is var[:dyn_lds_bytes[:chunk]].  Variant bits (kern_fir_ols_os.hip): 1
+A case is var[:dyn_lds_bytes[:chunk]].  OLS_BURST=B times B back-to-back calls per
+sample (the bench's sustained regime) instead of one isolated call.  Variant bits (kern_fir_ols_os.hip): 1
 wave-level sync for the two wave-local phase boundaries; 2 no HBM traffic
 (ablation); 4 HBM traffic only (ablation); 16 XCDs interleaved in runs of
 `chunk` segments instead of contiguous eighths.  dyn_lds pins occupancy
@@ -71,6 +72,7 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
         f.execute_block_device(d_in, n, d_out, s)
     torch.cuda.synchronize()
     rng = np.random.default_rng(1)
+    burst = int(os.environ.get("OLS_BURST", "1"))  # > 1: back-to-back calls per sample (sustained, bench-like)
     times = {v: [] for v in variants}
     order = list(variants)
     for i in range(rounds):
@@ -80,10 +82,11 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
             L.sdsp_lab_set_ols_variant(*v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            f.execute_block_device(d_in, n, d_out, s)
+            for _ in range(burst):
+                f.execute_block_device(d_in, n, d_out, s)
             e1.record(s)
             torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1))
+            times[v].append(e0.elapsed_time(e1) / burst)
     res = {"var%d:%d:%d" % v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "frac_of_8TBps": 16.0 * n / (np.median(t) * 1e-3) / 8e12,
                        "rel_diff_vs_var0": diff.get(v)} for v, t in times.items()}
