@@ -111,11 +111,20 @@ def test_chan_asm_checker_flags_unsafe_code():
     loop = [(base + 8 * i, mn, ops, None) for i, (mn, ops) in enumerate(
         [("buffer_load_dwordx2", f" v[{2 * i}:{2 * i + 1}], v40, s[0:3], 0 offen") for i in range(8)]
         + [("buffer_store_dwordx2", " v[20:21], v41, s[4:7], 0 offen nt")] * 16
-        + [("s_waitcnt", " vmcnt(16)"), ("v_mov_b64_e32", " v[30:31], v[2:3]"), ("s_endpgm", "")])]
+        + [("s_waitcnt", " vmcnt(16)"), ("v_mov_b64_e32", " v[30:31], v[14:15]"), ("s_endpgm", "")])]
     assert m.check_kernel(pro + loop) == []
     early = loop[:8] + loop[8:8 + 15] + loop[24:]  # one store short: vmcnt(16) no longer covers
     assert m.check_kernel(pro + early)
-    use = loop[:8] + [(0x200, "v_add_f32_e32", " v50, v3, v4", None)] + loop[8:]
+    use = loop[:8] + [(0x200, "v_add_f32_e32", " v50, v3, v4", None)] + loop[8:]  # before any wait
     assert m.check_kernel(pro + use)
     spill = pro + loop[:-1] + [(0x300, "scratch_store_dword", " off, v1, s0", None), loop[-1]]
     assert m.check_kernel(spill)
+    # per load: a wait that covers only the group's first loads releases only their registers
+    two = [(0x400 + 8 * i, "buffer_load_dwordx2", f" v[{2 * i}:{2 * i + 1}], v40, s[0:3], 0 offen", None)
+           for i in range(16)]
+    wait8 = [(0x500, "s_waitcnt", " vmcnt(8)", None)]
+    first = [(0x508, "v_mov_b64_e32", " v[50:51], v[2:3]", None)]
+    second = [(0x508, "v_mov_b64_e32", " v[50:51], v[18:19]", None)]
+    end = [(0x510, "s_waitcnt", " vmcnt(0)", None), (0x518, "s_endpgm", "", None)]
+    assert m.check_kernel(pro + two + wait8 + first + end) == []
+    assert m.check_kernel(pro + two + wait8 + second + end)

@@ -126,49 +126,48 @@ def check_kernel(insns):
     if len(groups) < 2:
         probs.append(f"expected the prologue and loop asm-load groups, found {len(groups)}")
     for g0, g1 in groups:
-        dest = set()
-        for k in range(g0, g1):
-            dest |= vregs(insns[k][2].split(",")[0])
-        # DFS over (instruction index, VMEM ops issued since the loads): a path is done at a
-        # wait vmcnt(N) with N <= issued (the loads have landed) or at s_endpgm
-        stack, seen = [(g1, 0, (), None)], set()
-        while stack:
-            k, cnt, cst, vcc = stack.pop()
-            consts = dict(cst)
-            while k < len(insns):
-                key = (k, cnt, tuple(sorted(consts.items())), vcc)
-                if key in seen:
-                    break
-                seen.add(key)
-                a, mn, ops, tgt = insns[k]
-                if mn == "s_waitcnt" and "vmcnt(" in ops:
-                    n = int(re.search(r"vmcnt\((\d+)\)", ops).group(1))
-                    if n <= cnt:
-                        break  # covered
-                if mn == "s_endpgm":
-                    break
-                used = vregs(ops) & dest
-                if used:
-                    probs.append(f"group at {insns[g0][0]:#x}: v{sorted(used)} used at {a:#x} ({mn}) after "
-                                 f"{cnt} VMEM ops, before a covering wait")
-                    break
-                if mn.startswith(VMEM):
-                    cnt = min(cnt + 1, 64)
-                if mn == "s_branch":
-                    k = index[tgt]
-                    continue
-                if mn.startswith(BRANCH_COND) and tgt is not None:
-                    taken = {"s_cbranch_vccnz": {0: False, "nz": True}, "s_cbranch_vccz": {0: True, "nz": False}}
-                    t = taken.get(mn, {}).get(vcc)
-                    if t is True:
+        for ld in range(g0, g1):  # each load on its own: a wait may cover only the group's first loads
+            dest = vregs(insns[ld][2].split(",")[0])
+            # DFS over (instruction index, VMEM ops issued since the load): a path is done at a
+            # wait vmcnt(N) with N <= issued (the load has landed) or at s_endpgm
+            stack, seen = [(ld + 1, 0, (), None)], set()
+            while stack:
+                k, cnt, cst, vcc = stack.pop()
+                consts = dict(cst)
+                while k < len(insns):
+                    key = (k, cnt, tuple(sorted(consts.items())), vcc)
+                    if key in seen:
+                        break
+                    seen.add(key)
+                    a, mn, ops, tgt = insns[k]
+                    if mn == "s_waitcnt" and "vmcnt(" in ops:
+                        n = int(re.search(r"vmcnt\((\d+)\)", ops).group(1))
+                        if n <= cnt:
+                            break  # covered
+                    if mn == "s_endpgm":
+                        break
+                    used = vregs(ops) & dest
+                    if used:
+                        probs.append(f"load at {insns[ld][0]:#x}: v{sorted(used)} used at {a:#x} ({mn}) after "
+                                     f"{cnt} VMEM ops, before a covering wait")
+                        break
+                    if mn.startswith(VMEM):
+                        cnt = min(cnt + 1, 64)
+                    if mn == "s_branch":
                         k = index[tgt]
                         continue
-                    if t is None:
-                        stack.append((index[tgt], cnt, tuple(sorted(consts.items())), vcc))
+                    if mn.startswith(BRANCH_COND) and tgt is not None:
+                        taken = {"s_cbranch_vccnz": {0: False, "nz": True}, "s_cbranch_vccz": {0: True, "nz": False}}
+                        t = taken.get(mn, {}).get(vcc)
+                        if t is True:
+                            k = index[tgt]
+                            continue
+                        if t is None:
+                            stack.append((index[tgt], cnt, tuple(sorted(consts.items())), vcc))
+                        k += 1
+                        continue
+                    consts, vcc = step_consts(mn, ops, consts, vcc)
                     k += 1
-                    continue
-                consts, vcc = step_consts(mn, ops, consts, vcc)
-                k += 1
     return probs
 
 
