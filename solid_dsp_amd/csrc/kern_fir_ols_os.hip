@@ -29,7 +29,9 @@
 //    (row offsets in SGPRs, no address arithmetic in VGPRs);
 //  * no twiddle tables in LDS or per-lane tables in registers: W4096^(t k) =
 //    D_{k>>2} C_{k&3} and W256^(l k) = F_{k>>2} E_{k&3} from per-lane bases
-//    (3 + 3 float4 from L2), the spectrum slice of P3 loaded from L2 in P2.
+//    (C1, D1, E1, F1: two float4 from L2; C2 = C1 C1, C3 = C2 C1, ...), the
+//    spectrum slice of P3 loaded from L2 in P2;
+//  * nontemporal input loads and stores (the stream is read and written once).
 //
 // LDS image: element (r, c) at r * 272 + c + (c >> 4) (one 8-byte pad per
 // 16-column block; rows 544 dwords apart, i.e. opposite halves of the 64
@@ -87,8 +89,8 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss);
 // ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
 // twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores; 16384
-// nontemporal input loads; 32768 two of the six twiddle bases loaded, the rest as their
-// products (results within rounding of the product kernel's).
+// plain (not nontemporal) input loads; 32768 all six twiddle bases loaded (the round-3 form;
+// 49152 = the round-3 kernel).
 template <int ABL>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -103,7 +105,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     for (int i = 0; i < 16; ++i) {
         const int r = (ABL & 256) ? 15 - i : i;
         if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
-        else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, (ABL & 16384) ? 2 : 0));
+        else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, (ABL & 16384) ? 0 : 2));
     }
     if constexpr (ABL & 4) {
         // every row's load in flight before the first store, as in the transform (without this
@@ -129,12 +131,13 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         }
     };
     f2 Cb[3], Da[3], Eb[3], Fa[3];
-    if constexpr ((ABL & 32768) != 0) {
-        // lab: the first power of each base from L2, the others as products (W^2 = W W, ...)
-        auto tab2 = [&](int lane, int off) {
-            return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rt, 16 * lane, off, 0));
-        };
-        const f2 c1 = tab2(t, 0), d1 = tab2(t, 4096 + 8), e1 = tab2(lo4, 12288), f1 = tab2(lo4, 12544 + 8);
+    if constexpr ((ABL & (32768 | 4096)) == 0) {
+        // the first power of each base from L2 ({C1, D1} per column, {E1, F1} per row: two
+        // 16-byte loads where the six-base form takes six), the others as products (W^2 = W W,
+        // W^3 = W^2 W): a third of the table traffic per segment, results within rounding of the
+        // six-base form (rel-RMS 2.2e-7 between the two on cfg2)
+        const float4 cd = tab(t, 16 * kOlsOsTabCD), ef = tab(lo4, 16 * kOlsOsTabEF);
+        const f2 c1 = f2{cd.x, cd.y}, d1 = f2{cd.z, cd.w}, e1 = f2{ef.x, ef.y}, f1 = f2{ef.z, ef.w};
         const f2 c2 = pmul(c1, c1), d2 = pmul(d1, d1), e2 = pmul(e1, e1), f2_ = pmul(f1, f1);
         Cb[0] = c1, Cb[1] = c2, Cb[2] = pmul(c2, c1);
         Da[0] = d1, Da[1] = d2, Da[2] = pmul(d2, d1);

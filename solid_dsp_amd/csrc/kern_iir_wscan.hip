@@ -144,6 +144,16 @@ __device__ __forceinline__ void sys_matvec(const C* __restrict__ P, const I (&x)
 }
 
 using v4u = unsigned __attribute__((ext_vector_type(4)));
+typedef float ws_f2 __attribute__((ext_vector_type(2)));
+
+// {acc.x + s.x v[HI], acc.y + s.y v[HI]}: one v_pk_fma_f32, s an SGPR pair, v[HI] broadcast to
+// both lanes by op_sel; per lane the fused multiply-add of fmac_
+template <int HI> __device__ __forceinline__ ws_f2 pk_fma_sb(ws_f2 s, ws_f2 v, ws_f2 acc) {
+    ws_f2 r;
+    if constexpr (HI == 0) asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,0,1]" : "=v"(r) : "s"(s), "v"(v), "v"(acc));
+    else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "s"(s), "v"(v), "v"(acc));
+    return r;
+}
 
 template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / sizeof(I)]) {
     v4u v;
@@ -162,7 +172,8 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // LAB selects compile-time variants for in-process A/B runs (tools/lab/iir_lab.hip; the product
 // kernels are LAB = 0): ablations 1 no zero-state run, 2 no scan, 4 no correction, 8 no HBM
 // loads, 16 no HBM stores; variants 32 plain (not nontemporal) loads, 64 plain stores, 128
-// nontemporal stores (the round-3 product; the product's interior stores are write-through)
+// nontemporal stores (the round-3 product; the product's interior stores are write-through), 256
+// the scalar correction (the round-3 arithmetic; real f32)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -173,6 +184,10 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     constexpr int D = ND ? ND : 2 * S;
     constexpr int B = ws_chunk<I, CB>::B;
     constexpr bool RERUN = FORM == 1, PF = FORM != 2;
+    // real f32: the correction in packed math over sample pairs (Cr in the [B/2][D][2] layout,
+    // runtime_iir.cpp scan_tables); LAB 256: the scalar form over the same layout
+    constexpr bool kPairCr = std::is_same<I, float>::value && std::is_same<C, float>::value;  // the layout
+    constexpr bool kPackedCr = kPairCr && D % 2 == 0 && (LAB & 256) == 0;
     constexpr int E = 16 / (int)sizeof(I);  // samples per 16-byte vector
     constexpr int kRowBytes = WsGeom<CB>::kRowBytes, kVecPerRow = WsGeom<CB>::kVecPerRow;
     constexpr int kSlabBytes = WsGeom<CB>::kSlabBytes;
@@ -340,18 +355,44 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
             }
         } else {
+            [[maybe_unused]] ws_f2 initp[kPackedCr ? D / 2 : 1];
+            if constexpr (kPackedCr) {
+#pragma unroll
+                for (int d = 0; d < D; d += 2) initp[d / 2] = ws_f2{init[d], init[d + 1]};
+            }
 #pragma unroll 2
             for (int o = 0; o < kVecPerRow && !(lab & 4); ++o) {
                 I e[E];
                 const v4u val = *reinterpret_cast<const v4u*>(row + o * 16);
                 __builtin_memcpy(e, &val, 16);
+                if constexpr (kPackedCr) {
+                    // real f32: samples (2q, 2q + 1) of the chunk in one v_pk_fma_f32 per state, the
+                    // pair {Cr[2q][d], Cr[2q+1][d]} an SGPR operand (host layout [B/2][D][2]) and
+                    // init[d] broadcast by op_sel -- per sample the fmas below, bit for bit, in half
+                    // the instructions (cfg3 sustained 1.664 -> 1.643 ms; the same packing of the
+                    // lane scan and a skewed packed zero-state run measured slower)
+                    const ws_f2* crp = reinterpret_cast<const ws_f2*>(Cr) + (o * (E / 2)) * D;
 #pragma unroll
-                for (int i = 0; i < E; ++i) {
-                    // Cr row of sample o E + i: wave-uniform, read through the scalar cache into
-                    // SGPR operands (an LDS broadcast read costs a full ds_read_b128 per 4 values)
-                    const C* cr = Cr + (o * E + i) * D;
+                    for (int q = 0; q < E / 2; ++q) {
+                        ws_f2 acc = {e[2 * q], e[2 * q + 1]};
 #pragma unroll
-                    for (int d = 0; d < D; ++d) e[i] = fmac_(e[i], cr[d], init[d]);
+                        for (int d = 0; d < D; d += 2) {
+                            acc = pk_fma_sb<0>(crp[q * D + d], initp[d / 2], acc);
+                            acc = pk_fma_sb<1>(crp[q * D + d + 1], initp[d / 2], acc);
+                        }
+                        e[2 * q] = acc.x;
+                        e[2 * q + 1] = acc.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < E; ++i) {
+                        // Cr row of sample o E + i: wave-uniform, read through the scalar cache into
+                        // SGPR operands (an LDS broadcast read costs a full ds_read_b128 per 4 values)
+                        const C* cr = Cr + (o * E + i) * D;
+                        if constexpr (kPairCr) cr = Cr + ((o * E + i) / 2) * 2 * D + ((o * E + i) & 1);
+#pragma unroll
+                        for (int d = 0; d < D; ++d) e[i] = fmac_(e[i], cr[kPairCr ? 2 * d : d], init[d]);
+                    }
                 }
                 *reinterpret_cast<v4u*>(row + o * 16) = to_v4<I>(e);
             }
@@ -559,7 +600,11 @@ sos_wscan2_kernel(const float* __restrict__ x, float* __restrict__ y, const floa
     float* sP = reinterpret_cast<float*>(lds_raw + kWsWaves * kSlabBytes);
     float* sCr = sP + 7 * D * D;
     for (int i = threadIdx.x; i < 7 * D * D; i += kWsThreads) sP[i] = P[i];
-    for (int i = threadIdx.x; i < B * D; i += kWsThreads) sCr[i] = Cr[i];
+    // Cr arrives in the [B/2][D][2] layout of the real-f32 tables (scan_tables)
+    for (int j = threadIdx.x; j < B * D; j += kWsThreads) {
+        const int i = j / D, d = j % D;
+        sCr[j] = Cr[((i / 2) * D + d) * 2 + (i & 1)];
+    }
     __syncthreads();
 
     const int ch = blockIdx.y;

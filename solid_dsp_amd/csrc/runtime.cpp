@@ -207,7 +207,8 @@ int ols_build(sdsp_fir* h) {
              "copy packed tables");
     // one-shot kernel (kern_fir_ols_os.hip): per column c the twiddle bases C_b = W4096^(b c),
     // D_a = W4096^(4 a c) (b, a = 1..3) as float4 [q][c] = (C1 C2 | C3 D1 | D2 D3), then per
-    // row l the W256 bases E_b = W256^(b l), F_a = W256^(4 a l) as float4 [768 + 16 q + l]
+    // row l the W256 bases E_b = W256^(b l), F_a = W256^(4 a l) as float4 [768 + 16 q + l], then
+    // the first powers alone (kOlsOsTabCD, kOlsOsTabEF: the default kernel's two loads)
     std::vector<float> os(4 * kOlsOsTabF4);
     auto put = [&](size_t f4, int half, long long m, int nn) {
         const double ang = -2.0 * M_PI * (double)(m % nn) / nn;
@@ -221,6 +222,14 @@ int ols_build(sdsp_fir* h) {
         put(256 + c, 1, 4LL * c, 4096);
         put(512 + c, 0, 8LL * c, 4096);
         put(512 + c, 1, 12LL * c, 4096);
+    }
+    for (int c = 0; c < 256; ++c) {  // {C1, D1} per column
+        put(kOlsOsTabCD + c, 0, c, 4096);
+        put(kOlsOsTabCD + c, 1, 4LL * c, 4096);
+    }
+    for (int l = 0; l < 16; ++l) {  // {E1, F1} per row
+        put(kOlsOsTabEF + l, 0, l, 256);
+        put(kOlsOsTabEF + l, 1, 4LL * l, 256);
     }
     for (int l = 0; l < 16; ++l) {
         put(768 + l, 0, l, 256);

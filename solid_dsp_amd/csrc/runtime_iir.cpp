@@ -320,7 +320,13 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
         for (int i = 0; i < B; ++i) resp[(size_t)i * D + d] = out[i];
     }
     std::vector<unsigned char> Cr;
-    for (double v : resp) push_coef(Cr, v, h->dtype);
+    if (h->dtype == 0 && B % 2 == 0) {  // real f32: sample pairs, [B/2][D][2] (packed correction)
+        for (int q = 0; q < B / 2; ++q)
+            for (int d = 0; d < D; ++d)
+                for (int i = 2 * q; i < 2 * q + 2; ++i) push_coef(Cr, resp[(size_t)i * D + d], h->dtype);
+    } else {
+        for (double v : resp) push_coef(Cr, v, h->dtype);
+    }
     IIR_TRY(dCr->ensure(Cr.size()), "alloc Cr");
     IIR_TRY(hipMemcpy(dCr->p, Cr.data(), Cr.size(), hipMemcpyHostToDevice), "copy Cr");
     return SDSP_OK;

@@ -32,7 +32,10 @@ constexpr int kOlsOneShot = 0;     // interior segments: one-shot XCD-ordered ke
 constexpr int kOlsPersistent = 1;  // persistent packed kernel, kOlsSegsPerBlock segments per workgroup
 constexpr int kOlsScalar = 2;      // scalar persistent kernel for every segment (kern_fir_ols.hip)
 constexpr int kOlsSegsPerBlock = 16;
-constexpr int kOlsOsTabF4 = 768 + 48;  // W4096 column bases [3][256], W256 row bases [3][16]
+// W4096 column bases [3][256], W256 row bases [3][16], then the first powers alone: {C1, D1}
+// per column [256] and {E1, F1} per row [16] (kern_fir_ols_os.hip, runtime.cpp ols_build)
+constexpr int kOlsOsTabCD = 768 + 48, kOlsOsTabEF = kOlsOsTabCD + 256;
+constexpr int kOlsOsTabF4 = kOlsOsTabEF + 16;
 
 struct OlsPlan {
     void* d_H;    // [256][16] c32: H[k0 + 16 k1 + 256 k2] / N * scale, row t = 16 k0 + k1

@@ -21,6 +21,7 @@ for s in ${STEPS:-pytest}; do
         olsab) OLS_ROUNDS=${ROUNDS:-15} OLS_CASES=${OLS_CASES:-0,256,4,260} run olsab 600 python -u tools/ols_lab.py ;;
         olsburst) OLS_BURST=${BURST:-20} OLS_ROUNDS=${BROUNDS:-6} OLS_CASES=${OLS_CASES:-0,256,4,260} run olsburst 600 python -u tools/ols_lab.py ;;
         iirab) IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirab 600 python -u tools/iir_ab.py ;;
+        iirburst) IIR_BURST=${BURST:-20} IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirburst 600 python -u tools/iir_ab.py ;;
         chanab) run chanab 600 python -u tools/chan_ab.py ;;
         copyprobe) run copyprobe 300 tools/_build/copy_shape_probe ;;
         fftslice) run fftslice 300 python -u tools/fft_slice_ab.py ;;

@@ -52,6 +52,7 @@ def main(rounds=8, log2n=30):
     for _ in range(40):  # clocks settle
         variants[keys[-1]].execute_block_device(d_in, n, d_out, s)
     rng = np.random.default_rng(0)
+    burst = int(os.environ.get("IIR_BURST", "1"))  # > 1: back-to-back calls per sample (sustained, bench-like)
     for _ in range(rounds):
         for k in rng.permutation(keys):
             f = variants[k]
@@ -59,10 +60,11 @@ def main(rounds=8, log2n=30):
                 sd.lib().sdsp_lab_set_iir_ablation(abl[k])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            f.execute_block_device(d_in, n, d_out, s)
+            for _ in range(burst):
+                f.execute_block_device(d_in, n, d_out, s)
             e1.record(s)
             torch.cuda.synchronize()
-            times[k].append(e0.elapsed_time(e1))
+            times[k].append(e0.elapsed_time(e1) / burst)
     res = {k: {"median_ms": float(np.median(v)), "GBps": 8.0 * n / (np.median(v) * 1e-3) / 1e9}
            for k, v in times.items()}
     res["rel_rms_between"] = agree

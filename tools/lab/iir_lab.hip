@@ -2,7 +2,7 @@
 // libsdsp.so): the product source compiled unchanged (its launcher renamed) plus
 // a launcher that runs sos_wscan_kernel<..., LAB> on real-f32 4-section warm-up
 // scans (the cfg3 shape) for the ablation set by sdsp_lab_set_iir_ablation
-// (tools/iir_ab.py).  LAB bits are documented at sos_wscan_kernel; bits 8-11 of
+// (tools/iir_ab.py).  LAB bits are documented at sos_wscan_kernel; bits 12-15 of
 // the ablation value force the tiles per wave.  tools/lab.mk links it in place of
 // the product object.
 #define launch_iir_wscan launch_iir_wscan_product
@@ -22,6 +22,8 @@ template <int CB>
 static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw) {
     switch (ab) {
         case 1: return lab_cfg3<CB, 1>(a, st, tpw);
+        case 5: return lab_cfg3<CB, 5>(a, st, tpw);
+        case 6: return lab_cfg3<CB, 6>(a, st, tpw);
         case 2: return lab_cfg3<CB, 2>(a, st, tpw);
         case 4: return lab_cfg3<CB, 4>(a, st, tpw);
         case 7: return lab_cfg3<CB, 7>(a, st, tpw);
@@ -32,12 +34,14 @@ static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw)
         case 64: return lab_cfg3<CB, 64>(a, st, tpw);
         case 128: return lab_cfg3<CB, 128>(a, st, tpw);
         case 136: return lab_cfg3<CB, 136>(a, st, tpw);
+        case 256: return lab_cfg3<CB, 256>(a, st, tpw);
+        case 280: return lab_cfg3<CB, 280>(a, st, tpw);
         default: return lab_cfg3<CB, 0>(a, st, tpw);
     }
 }
 
 hipError_t launch_iir_wscan(int dtype, const IirArgs& a, hipStream_t st) {
-    const int ab = g_iir_lab & 255, tpw = (g_iir_lab >> 8) & 15;
+    const int ab = g_iir_lab & 4095, tpw = (g_iir_lab >> 12) & 15;
     if ((ab || tpw) && dtype == 0 && a.sections == 4 && a.Mi == 1 && a.Md == 1 && a.wc > 0 && a.n > 0) {
         if (a.ws_variant == 1) return lab_cfg3_ab<128>(a, st, ab, tpw);
         if (a.ws_variant == 0) return lab_cfg3_ab<256>(a, st, ab, tpw);
