@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--shard", default="channel", choices=["channel", "time"],
                    help="configs 2 and 4: independent channels per rank (default), or one long stream "
                         "time-sharded (rank r filters inputs [r n, (r+1) n) after an (L-1)-input halo)")
+    p.add_argument("--settle-ms", type=float, default=150.0,
+                   help="untimed steps of the workload before the warm-up, in ms of device time (0: none)")
     p.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                    help="kernel-variant knob on the workload's handle, e.g. FFT_WAVE1024=2 "
                         "(SDSP_TUNE_<NAME>, include/sdsp.h); A/B runs only, the default line uses none")
@@ -1220,7 +1222,7 @@ def main():
     # brings the device out of its idle clocks (~0.3 s of streaming) so the
     # workload's own warm-up steps are not spent on the clock ramp
     copy_gbps = stream_copy_gbps(torch, sd)
-    settled = settle(w, stream, torch)
+    settled = settle(w, stream, torch, ms=args.settle_ms) if args.settle_ms > 0 else None
 
     for _ in range(args.warmup):
         w.step(stream)

@@ -14,11 +14,11 @@ declare -A KERN=([1]=fir_direct [2]=fir_ols_os [3]=sos_wscan [4]=decim_poly [5]=
 if [ -z "$SKIP_TESTS" ]; then run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider; fi
 for c in ${CONFIGS:-2 3 4 5}; do
   run bench_cfg$c 300 python bench.py --config $c --steps 20 --warmup 5
-  run prof_cfg$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg$c -o run -- python bench.py --config $c --steps 20 --warmup 5 --no-cpu --no-parity
-  python tools/prof_summary.py gpurun_out/${TAG}_prof_cfg$c ${KERN[$c]} --skip 5 --take 20 --out gpurun_out/${TAG}_kernel_timed_cfg$c.json > /dev/null 2>&1 || echo "prof_summary cfg$c failed"
+  run prof_cfg$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg$c -o run -- python bench.py --config $c --steps 20 --warmup 5 --no-cpu --no-parity --no-dropin
+  python tools/prof_summary.py gpurun_out/${TAG}_prof_cfg$c ${KERN[$c]} --last 20 --out gpurun_out/${TAG}_kernel_timed_cfg$c.json > /dev/null 2>&1 || echo "prof_summary cfg$c failed"
   if [ -z "$SKIP_PMC" ]; then
-    run pmc_fetch_cfg$c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity
-    run pmc_write_cfg$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity
+    run pmc_fetch_cfg$c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity --settle-ms 0
+    run pmc_write_cfg$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity --settle-ms 0
   fi
 done
 echo done
