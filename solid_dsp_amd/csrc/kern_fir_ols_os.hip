@@ -105,7 +105,10 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     for (int i = 0; i < 16; ++i) {
         const int r = (ABL & 256) ? 15 - i : i;
         if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
-        else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, (ABL & 16384) ? 0 : 2));
+        else if constexpr ((ABL & 16384) != 0)
+            v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+        else  // nontemporal (aux 2)
+            v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 2));
     }
     if constexpr (ABL & 4) {
         // every row's load in flight before the first store, as in the transform (without this
