@@ -157,9 +157,8 @@ typedef enum {
     SDSP_TUNE_FFT_GROUP = 18,      /* four-step passes on the generic pass kernel: at most this many
                                       transforms per workgroup (1..64, default 4) */
     SDSP_TUNE_FFT_WAVE1024 = 19,   /* four-step passes of 1024 points (c32): 16 (default) pipelined persistent
-                                      wave-FFT kernel, 2 the same with 8-transform groups (two workgroups per
-                                      CU) on the column pass, 1 / 8 one-shot with 16 / 8 transforms per
-                                      workgroup, 0 the generic pass kernel */
+                                      wave-FFT kernel, 1 / 8 one-shot with 16 / 8 transforms per workgroup,
+                                      0 the generic pass kernel */
     SDSP_TUNE_ACORR_KERNEL = 20,   /* AutoCorrelator: 0 (default) pipelined kernel on interior tiles (delay
                                       and window <= 128), one-shot kernel elsewhere; 1 the one-shot kernel
                                       everywhere, delayed input staged in LDS (delay <= 256); 2 the one-shot

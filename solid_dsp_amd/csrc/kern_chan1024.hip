@@ -597,8 +597,9 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 }
 
 // Persistent, software-pipelined form of the pass above (the default): grid = one
-// 1024-thread workgroup per CU (TPB = 16; TPB = 8: two 512-thread workgroups per CU),
-// workgroup b runs groups b, b + G, b + 2G, ... of TPB transforms.  The loads of the next group are issued
+// 1024-thread workgroup per CU, workgroup b runs groups b, b + G, b + 2G, ... of TPB = 16
+// transforms (8-transform groups in two 512-thread workgroups per CU measured 2.25 against
+// 1.80 ms on cfg8, profiles/r04/lab/r04b_tune8_*.log).  The loads of the next group are issued
 // into registers BEFORE the current group's FFT and stores, so each CU's HBM
 // queue never drains while it transforms (the one-shot kernel alternated: load,
 // barrier, FFT, barrier, store, with one 141 KB workgroup per CU and nothing else
@@ -612,19 +613,15 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
                                                   const cf* __restrict__ tw, const cf* __restrict__ twx,
                                                   long long count, long long G, long long S0, long long S1,
                                                   long long Si, long long T1, long long So) {
-    static_assert(TPB == 16 || TPB == 8, "16 or 8 transforms per workgroup");
-    constexpr int kT = 64 * TPB, kLog = TPB == 16 ? 4 : 3;
+    static_assert(TPB == 16, "16 transforms per workgroup");
+    constexpr int kT = 64 * TPB, kLog = 4;
     constexpr int kPre = PRE;
     __shared__ cf stw[kM];
     __shared__ cf sbuf[TPB * kPassBuf];
     __shared__ cf ktab[TW ? TPB * 16 : 1];
     const int t = threadIdx.x, L = t & 63, w = t >> 6;
     const long long ngroups = count / TPB;
-    if constexpr (kT == kM) {
-        stw[t] = tw[t];
-    } else {
-        for (int i = t; i < kM; i += kT) stw[i] = tw[i];
-    }
+    stw[t] = tw[t];
     auto twx_at = [&](long long m) -> cf {
         const unsigned u = (unsigned)(m & ((1 << 20) - 1));
         return cmul(twx[1024 + (u >> 10)], twx[u & 1023]);
@@ -639,9 +636,7 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
     };
     // element k of thread t sits at lane offset + k * (scalar stride): buffer loads and
     // stores with one offset VGPR (64-bit addresses per element spill the pipeline's
-    // registers).  cfast: c = t & (TPB - 1), i = (t >> kLog) + 64 k; else (TPB = 16 only)
-    // c = k, i = t.
-    static_assert(TPB == 16 || (CFAST && OFAST), "8-transform groups: the unit-stride (column) pass only");
+    // registers).  cfast: c = t & (TPB - 1), i = (t >> kLog) + 64 k; else c = k, i = t.
     const unsigned in_lane = (unsigned)(cfast ? ((t & (TPB - 1)) + (long long)(t >> kLog) * Si) : (long long)t * Si) * 8u;
     const unsigned in_k = (unsigned)(cfast ? 64 * Si : S1) * 8u;
     const unsigned out_lane = (unsigned)(ofast ? ((t & (TPB - 1)) + (long long)(t >> kLog) * So) : (long long)t * So) * 8u;
@@ -717,17 +712,6 @@ fft1024_pipe_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
     fft1024_pipe_body<INV, TW, CFAST, OFAST, 16>(x, y, tw, twx, count, G, S0, S1, Si, T1, So);
 }
 
-// 8-transform groups on the unit-stride (column) pass: two 512-thread workgroups per CU, so at
-// most 128 VGPRs (4 waves per SIMD).  Launched with 512 threads; the 1024 bound is what makes
-// the compiler budget for 4 waves per SIMD (its LDS model admits one 75 KB workgroup per CU)
-template <bool INV, bool TW>
-__global__ void __launch_bounds__(1024)
-fft1024_pipe8_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __restrict__ tw,
-                     const cf* __restrict__ twx, long long count, long long G, long long S0, long long S1,
-                     long long Si, long long T1, long long So) {
-    fft1024_pipe_body<INV, TW, true, true, 8>(x, y, tw, twx, count, G, S0, S1, Si, T1, So);
-}
-
 }  // namespace
 
 // M = 1024, complex f32, K <= 8 taps per branch; false = not applicable.  LAB: chan1024_kernel
@@ -783,33 +767,16 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
 
 // four-step pass of L = 1024 on the wave FFT; false = not applicable
 bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
-    // p.wave1024 (SDSP_TUNE_FFT_WAVE1024): 16 (default) the pipelined persistent kernel, 2 the same
-    // with 8-transform groups (two 512-thread workgroups per CU) on the unit-stride column pass,
-    // 1 the one-shot kernel with 16 transforms per workgroup, 8 one-shot with 8, 0 the generic
+    // p.wave1024 (SDSP_TUNE_FFT_WAVE1024): 16 (default) the pipelined persistent kernel, 1 the
+    // one-shot kernel with 16 transforms per workgroup, 8 one-shot with 8, 0 the generic
     // Stockham pass
-    const int tpb = p.wave1024 == 0 || p.wave1024 == 8 || p.wave1024 == 1 || p.wave1024 == 2 ? p.wave1024 : 16;
+    const int tpb = p.wave1024 == 0 || p.wave1024 == 8 || p.wave1024 == 1 ? p.wave1024 : 16;
     if (tpb == 0 || p.L != 1024 || p.count % 16 != 0 || p.G % 16 != 0) return false;
     if (!(p.S1 == 1 || p.Si == 1) || !(p.T1 == 1 || p.So == 1)) return false;
     if (p.Ntw && (p.Ntw != (1LL << 20) || !p.twx)) return false;
-    const bool pipe8 = tpb == 2 && p.S1 == 1 && p.T1 == 1;
-    if (tpb == 16 || tpb == 2) {
+    if (tpb == 16) {
         int dev = 0, cus = 256;  // (the current device's CU count)
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (pipe8) {
-            const long long groups = p.count / 8;
-            const dim3 g8((unsigned)(groups < 2LL * cus ? groups : 2LL * cus));
-#define SDSP_PIPE8(INV, TW)                                                                                       \
-    hipLaunchKernelGGL((fft1024_pipe8_kernel<INV, TW>), g8, dim3(512), 0, s, (const cf*)p.x,                      \
-                       (cf*)p.y, (const cf*)p.tw, (const cf*)p.twx, p.count, p.G, p.S0, p.S1, p.Si, p.T1, p.So)
-            if (p.inverse) {
-                if (p.Ntw) SDSP_PIPE8(true, true); else SDSP_PIPE8(true, false);
-            } else {
-                if (p.Ntw) SDSP_PIPE8(false, true); else SDSP_PIPE8(false, false);
-            }
-#undef SDSP_PIPE8
-            *err = hipGetLastError();
-            return true;
-        }
         const long long groups = p.count / 16;
         const dim3 g2((unsigned)(groups < cus ? groups : cus));
         const bool cf_ = p.S1 == 1, of_ = p.T1 == 1;

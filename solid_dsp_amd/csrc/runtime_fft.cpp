@@ -285,7 +285,7 @@ size_t sdsp_fft_len(const sdsp_fft* h) { return h ? h->N : 0; }
 int sdsp_fft_set_tuning(sdsp_fft* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     if (key == SDSP_TUNE_FFT_GROUP && value >= 1 && value <= 64) h->p2.group = value;
-    else if (key == SDSP_TUNE_FFT_WAVE1024 && (value == 0 || value == 1 || value == 2 || value == 8 || value == 16))
+    else if (key == SDSP_TUNE_FFT_WAVE1024 && (value == 0 || value == 1 || value == 8 || value == 16))
         h->p2.wave1024 = value;
     else return SDSP_E_INVALID_ARGUMENT;
     return SDSP_OK;

@@ -141,8 +141,7 @@ struct FftPass {
     const void* twx = nullptr;  // c32 [Tl | Th] inter-pass twiddle tables when Ntw = 2^20 (L = 1024 path)
     int group = 4;      // generic pass: at most this many transforms per workgroup (SDSP_TUNE_FFT_GROUP)
     int wave1024 = 16;  // L = 1024 c32 passes (SDSP_TUNE_FFT_WAVE1024): 16 pipelined persistent kernel,
-                        // 2 the same with 8-transform groups on the column pass, 1 / 8 one-shot with
-                        // 16 / 8 transforms per workgroup, 0 the generic pass
+                        // 1 / 8 one-shot with 16 / 8 transforms per workgroup, 0 the generic pass
 };
 // L = 1024, complex f32 pass on the wave FFT (kern_chan1024.hip); false = not applicable
 bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err);
