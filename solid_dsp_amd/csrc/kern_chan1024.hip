@@ -281,7 +281,9 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // = 5 / 6) halve / quarter the bytes a CU has in flight per round (R x 8 KB of loads and as
 // many of stores) and transform the round's frames on waves 0..R-1.
 // LAB selects compile-time variants for in-process A/B runs (tools/lab/chan_lab.hip; the
-// product kernels are LAB = 0): 1 no FFT, 2 no loads, 4 no stores (ablations); 8 / 16 odd
+// product kernels are LAB = 0): 1 no FFT, 2 no loads, 4 no stores (ablations; 1 and 4 issue fewer
+// than the sixteen stores per round that the PF / R = 8 form's vmcnt(16) wait counts on, so with
+// that form they are timing ablations only, their outputs invalid); 8 / 16 odd
 // workgroups start ~6.8 / ~3.4 us late; 32 plain stores; 64 nontemporal loads (16-byte and
 // guarded paths); 128 write-through (sc1) stores; 256 nontemporal round loads (the asm path).
 template <int K, int T, bool PF, int R = T / 64, int LAB = 0>
