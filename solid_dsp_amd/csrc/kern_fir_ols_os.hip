@@ -90,7 +90,8 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
 // twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores; 16384
 // plain (not nontemporal) input loads; 32768 all six twiddle bases loaded (the round-3 form;
-// 49152 = the round-3 kernel).
+// 49152 = the round-3 kernel); 131072 with 4: the HBM-only pattern in 16-byte lanes (the NCO
+// kernel's shape).
 template <int ABL>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
@@ -104,13 +105,27 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int r = (ABL & 256) ? 15 - i : i;
-        if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
+        if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
+        else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
         else if constexpr ((ABL & 16384) != 0)
             v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
         else  // nontemporal (aux 2)
             v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 2));
     }
-    if constexpr (ABL & 4) {
+    if constexpr ((ABL & 4) && (ABL & 131072)) {
+        // HBM-only with the NCO kernel's lane shape: the segment as eight 4 KB rows of 16-byte
+        // lanes (lane t: bytes 16 t + 4096 k), the halo's bytes not stored
+        typedef unsigned u4v __attribute__((ext_vector_type(4)));
+        u4v w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rx, 16 * t, 4096 * k, 2));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(w[k]));
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (4096 * k + 16 * t >= 2048 * h2) __builtin_amdgcn_raw_buffer_store_b128(w[k], ry, 16 * t, 4096 * k, 2);
+        return;
+    } else if constexpr (ABL & 4) {
         // every row's load in flight before the first store, as in the transform (without this
         // the compiler sinks each load into its store's `r >= h2` branch: one round trip per row)
 #pragma unroll

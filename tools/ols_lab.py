@@ -45,15 +45,19 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
     d_in = torch.empty(n, dtype=torch.complex64, device="cuda")
     L.sdsp_synth_f32_device(d_in.data_ptr(), 20250226, 0, 0, 2 * n, None)
     def parse(c):
+        if c == "nco":  # the NCO mix_down of the same buffer (cfg7's kernel), for a side-by-side
+            return (-1, 0, 1)
         f = (c.split(":") + ["", ""])[:3]
         return (int(f[0]), int(f[1] or 0), int(f[2] or 1))
     variants = [parse(c) for c in os.environ.get("OLS_CASES", "0,1,2,4").split(",")]
+    nco = sd.NCO()
+    nco.set_frequency(2 * np.pi * 0.0123)
     f = FIRFilter(h, np.float32(0.2), sample_dtype=np.complex64, algo=sd.ALGO_FFT)
     s = torch.cuda.current_stream()
     d_out = torch.empty_like(d_in)
     outs, diff = {}, {}
     for v in variants:
-        if v[0] < 256 and v[0] & 6:
+        if v[0] < 0 or (v[0] < 256 and v[0] & 6) or (v[0] & 131072):
             continue
         L.sdsp_lab_set_ols_variant(*v)
         f.reset()
@@ -79,15 +83,18 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
         print("round", i, flush=True)
         rng.shuffle(order)
         for v in order:
-            L.sdsp_lab_set_ols_variant(*v)
+            L.sdsp_lab_set_ols_variant(*(v if v[0] >= 0 else (0, 0, 1)))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(burst):
-                f.execute_block_device(d_in, n, d_out, s)
+                if v[0] < 0:
+                    nco.mix_block_device(d_in, n, d_out, down=True, precision=0, stream=s)
+                else:
+                    f.execute_block_device(d_in, n, d_out, s)
             e1.record(s)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / burst)
-    res = {"var%d:%d:%d" % v: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+    res = {("nco" if v[0] < 0 else "var%d:%d:%d" % v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "frac_of_8TBps": 16.0 * n / (np.median(t) * 1e-3) / 8e12,
                        "rel_diff_vs_var0": diff.get(v)} for v, t in times.items()}
     print(json.dumps(res, indent=1))
