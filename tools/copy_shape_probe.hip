@@ -48,6 +48,24 @@ __global__ void __launch_bounds__(256) copy_k(const char* __restrict__ a, char* 
     }
 }
 
+// 8-byte lanes in reversed order within each wave's 512 bytes (the channeliser's load shape:
+// lane t reads x[M - 1 - t] of a frame)
+template <int U, int LA, int SA, bool REVL, bool REVS>
+__global__ void __launch_bounds__(256) copy_rev_k(const char* __restrict__ a, char* __restrict__ b, unsigned long long bytes) {
+    const unsigned long long base = (unsigned long long)blockIdx.x * 256ull * U * 8;
+    const unsigned long long rem = bytes > base ? bytes - base : 0;
+    const unsigned nrec = (unsigned)(rem < 0x80000000ull ? rem : 0x80000000ull);
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc((void*)(a + base), (short)0, nrec, 0x00020000);
+    const auto rb = __builtin_amdgcn_make_buffer_rsrc((void*)(b + base), (short)0, nrec, 0x00020000);
+    const unsigned lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned lo = (wv * 64 + (REVL ? 63 - lane : lane)) * 8, so = (wv * 64 + (REVS ? 63 - lane : lane)) * 8;
+    u2 r[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) r[k] = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(ra, lo + 2048 * k, 0, LA));
+#pragma unroll
+    for (int k = 0; k < U; ++k) __builtin_amdgcn_raw_buffer_store_b64(r[k], rb, so + 2048 * k, 0, SA);
+}
+
 template <typename F>
 float time_ms(F f, int reps = 15) {
     hipEvent_t e0, e1;
@@ -77,6 +95,15 @@ void run(const char* a, char* b, unsigned long long bytes, const char* tag) {
                 2.0 * bytes / ms / 1e6);
 }
 
+template <int U, int LA, int SA, bool REVL, bool REVS>
+void run_rev(const char* a, char* b, unsigned long long bytes, const char* tag) {
+    const unsigned long long per = 256ull * U * 8;
+    const unsigned g = (unsigned)((bytes + per - 1) / per);
+    const float ms = time_ms([&] { copy_rev_k<U, LA, SA, REVL, REVS><<<g, 256>>>(a, b, bytes); });
+    std::printf("%-6s W= 8 U=%d load=%2d store=%2d rev_load=%d rev_store=%d  %8.4f ms  %7.1f GB/s\n", tag, U, LA, SA,
+                (int)REVL, (int)REVS, ms, 2.0 * bytes / ms / 1e6);
+}
+
 int main() {
     const unsigned long long maxb = 8ull << 30;
     char *a, *b;
@@ -97,6 +124,11 @@ int main() {
         run<8, 2, 0, 2>(a, b, s.bytes, s.tag);
         run<8, 2, 0, 16>(a, b, s.bytes, s.tag);
         run<8, 8, 0, 2>(a, b, s.bytes, s.tag);
+        run_rev<2, 0, 2, false, false>(a, b, s.bytes, s.tag);
+        run_rev<2, 0, 2, true, false>(a, b, s.bytes, s.tag);
+        run_rev<2, 0, 2, true, true>(a, b, s.bytes, s.tag);
+        run_rev<8, 0, 2, false, false>(a, b, s.bytes, s.tag);
+        run_rev<8, 0, 2, true, false>(a, b, s.bytes, s.tag);
         CK(hipDeviceSynchronize());
         std::fflush(stdout);
     }
