@@ -285,7 +285,8 @@ __device__ __forceinline__ void fft1024_chan(f2* __restrict__ buf, const ChanTw&
 // than the sixteen stores per round that the PF / R = 8 form's vmcnt(16) wait counts on, so with
 // that form they are timing ablations only, their outputs invalid); 8 / 16 odd
 // workgroups start ~6.8 / ~3.4 us late; 32 plain stores; 64 nontemporal loads (16-byte and
-// guarded paths); 128 write-through (sc1) stores; 256 nontemporal round loads (the asm path).
+// guarded paths); 128 write-through (sc1) stores; 256 plain (not nontemporal) round loads (the
+// asm path; the round-3 product).
 template <int K, int T, bool PF, int R = T / 64, int LAB = 0>
 __global__ void __launch_bounds__(T, T == 1024 ? 4 : 2)  // 1024 lanes: 4 waves per SIMD, 128 VGPRs
 chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const float* __restrict__ cb,
@@ -414,7 +415,9 @@ chan1024_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, const flo
                     typedef unsigned u4s __attribute__((ext_vector_type(4)));
                     const u4s rw = {(unsigned)a, (unsigned)(a >> 32) & 0xffffu, nrec, 0x00020000u};
                     f2 r;
-                    if constexpr ((LAB & 256) != 0)
+                    // nontemporal (the round's samples are read once): cfg5 sustained 0.388 ->
+                    // 0.376 ms (profiles/r04/lab/r04ab_chanburst.log, r04ac_chanburst.log)
+                    if constexpr ((LAB & 256) == 0)
                         asm volatile("buffer_load_dwordx2 %0, %1, %2, 0 offen nt"
                                      : "=v"(r)
                                      : "v"((unsigned)(f * kM + kM - 1 - t) * 8), "s"(rw)
@@ -610,7 +613,8 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 // contiguous runs.  Same arithmetic, element order and twiddles as
 // fft1024_pass_kernel<INV, TW, TPB> (bit-identical).  PRE: next-group loads issued before
 // the FFT (the rest after it).
-template <bool INV, bool TW, bool CFAST, bool OFAST, int TPB = 16, int PRE = 8>
+// LA / SA: the loads' / stores' cache policy (0 default, 2 nontemporal; lab variants)
+template <bool INV, bool TW, bool CFAST, bool OFAST, int TPB = 16, int PRE = 8, int LA = 0, int SA = 0>
 __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* __restrict__ y,
                                                   const cf* __restrict__ tw, const cf* __restrict__ twx,
                                                   long long count, long long G, long long S0, long long S1,
@@ -654,7 +658,7 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + ib), (short)0, ok ? 0x7fffffff : 0, 0x00020000);
 #pragma unroll
         for (int k = k0; k < k1; ++k)
-            v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, 0));
+            v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, LA));
     };
     long long grp = blockIdx.x;
     if (grp >= ngroups) return;  // uniform
@@ -697,7 +701,7 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
                 if (INV) wv.im = -wv.im;
                 r = cmul(r, wv);
             }
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, r), ry, out_lane, k * out_k, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, r), ry, out_lane, k * out_k, SA);
         }
         if (nxt >= ngroups) break;
         grp = nxt;
@@ -706,12 +710,12 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
 }
 
 
-template <bool INV, bool TW, bool CFAST, bool OFAST>
+template <bool INV, bool TW, bool CFAST, bool OFAST, int LA = 0, int SA = 0>
 __global__ void __launch_bounds__(1024)
 fft1024_pipe_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __restrict__ tw,
                     const cf* __restrict__ twx, long long count, long long G, long long S0, long long S1,
                     long long Si, long long T1, long long So) {
-    fft1024_pipe_body<INV, TW, CFAST, OFAST, 16>(x, y, tw, twx, count, G, S0, S1, Si, T1, So);
+    fft1024_pipe_body<INV, TW, CFAST, OFAST, 16, 8, LA, SA>(x, y, tw, twx, count, G, S0, S1, Si, T1, So);
 }
 
 }  // namespace
@@ -767,8 +771,10 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
     return try_launch_chan1024_t<0>(a, s, err);
 }
 
-// four-step pass of L = 1024 on the wave FFT; false = not applicable
-bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
+// four-step pass of L = 1024 on the wave FFT; false = not applicable.  LA / SA: the pipelined
+// kernel's load / store policy (0 = the product)
+template <int LA, int SA>
+bool try_launch_fft1024_pass_t(const FftPass& p, hipStream_t s, hipError_t* err) {
     // p.wave1024 (SDSP_TUNE_FFT_WAVE1024): 16 (default) the pipelined persistent kernel, 1 the
     // one-shot kernel with 16 transforms per workgroup, 8 one-shot with 8, 0 the generic
     // Stockham pass
@@ -783,7 +789,7 @@ bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
         const dim3 g2((unsigned)(groups < cus ? groups : cus));
         const bool cf_ = p.S1 == 1, of_ = p.T1 == 1;
 #define SDSP_PIPE4(INV, TW, C, O)                                                                                 \
-    hipLaunchKernelGGL((fft1024_pipe_kernel<INV, TW, C, O>), g2, dim3(1024), 0, s, (const cf*)p.x, (cf*)p.y,      \
+    hipLaunchKernelGGL((fft1024_pipe_kernel<INV, TW, C, O, LA, SA>), g2, dim3(1024), 0, s, (const cf*)p.x, (cf*)p.y, \
                        (const cf*)p.tw, (const cf*)p.twx, p.count, p.G, p.S0, p.S1, p.Si, p.T1, p.So)
 #define SDSP_PIPE(INV, TW)                                                                         \
     do {                                                                                           \
@@ -819,6 +825,10 @@ bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
 #undef SDSP_P1024
     *err = hipGetLastError();
     return true;
+}
+
+bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
+    return try_launch_fft1024_pass_t<0, 0>(p, s, err);
 }
 
 }  // namespace sdsp

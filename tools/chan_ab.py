@@ -56,6 +56,7 @@ def main(rounds=int(os.environ.get("CHAN_ROUNDS", "9"))):
     for _ in range(30):  # clocks settle
         variants[keys[-1]].execute_block_device(d_in, n, d_out, st)
     rng = np.random.default_rng(0)
+    burst = int(os.environ.get("CHAN_BURST", "1"))  # > 1: back-to-back calls per sample (sustained, bench-like)
     for _ in range(rounds):
         for k in rng.permutation(keys):
             f = variants[k]
@@ -63,10 +64,11 @@ def main(rounds=int(os.environ.get("CHAN_ROUNDS", "9"))):
                 sd.lib().sdsp_lab_set_chan_ablation(labs[k])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
-            f.execute_block_device(d_in, n, d_out, st)
+            for _ in range(burst):
+                f.execute_block_device(d_in, n, d_out, st)
             e1.record(st)
             torch.cuda.synchronize()
-            times[k].append(e0.elapsed_time(e1))
+            times[k].append(e0.elapsed_time(e1) / burst)
     res = {k: {"median_ms": float(np.median(v)), "GBps": 16.0 * S * n / (np.median(v) * 1e-3) / 1e9}
            for k, v in times.items()}
     res["rel_rms_between"] = agree

@@ -23,8 +23,10 @@ for s in ${STEPS:-pytest}; do
         iirab) IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirab 600 python -u tools/iir_ab.py ;;
         iirburst) IIR_BURST=${BURST:-20} IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirburst 600 python -u tools/iir_ab.py ;;
         chanab) run chanab 600 python -u tools/chan_ab.py ;;
+        chanburst) CHAN_BURST=${BURST:-40} run chanburst 600 python -u tools/chan_ab.py ;;
         copyprobe) run copyprobe 300 tools/_build/copy_shape_probe ;;
         fftslice) run fftslice 300 python -u tools/fft_slice_ab.py ;;
+        fftlab) run fftlab 300 python -u tools/fft_lab.py ;;
         nocopy*) run "$s" 300 python -u tools/steady_probe.py --config "${s#nocopy}" --steps 400 --no-copy ;;
         steady*) run "$s" 300 python -u tools/steady_probe.py --config "${s#steady}" --steps 400 ;;
         bench) run bench 300 python -u bench.py --steps 20 --warmup 5 ${BENCH_ARGS:-} ;;

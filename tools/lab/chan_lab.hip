@@ -4,12 +4,24 @@
 // sdsp_lab_set_chan_ablation (tools/chan_ab.py).  LAB bits are documented at
 // chan1024_kernel.  tools/lab.mk links it in place of the product object.
 #define try_launch_chan1024 try_launch_chan1024_product
+#define try_launch_fft1024_pass try_launch_fft1024_pass_product
 #include "kern_chan1024.hip"
 #undef try_launch_chan1024
+#undef try_launch_fft1024_pass
 
 namespace sdsp {
 
 static int g_chan_lab = 0;
+static int g_fft_policy = 0;  // 4-step L = 1024 passes: bit 0 nontemporal loads, bit 1 nontemporal stores
+
+bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
+    switch (g_fft_policy) {
+        case 1: return try_launch_fft1024_pass_t<2, 0>(p, s, err);
+        case 2: return try_launch_fft1024_pass_t<0, 2>(p, s, err);
+        case 3: return try_launch_fft1024_pass_t<2, 2>(p, s, err);
+        default: return try_launch_fft1024_pass_t<0, 0>(p, s, err);
+    }
+}
 
 bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
     switch (g_chan_lab) {
@@ -29,7 +41,10 @@ bool try_launch_chan1024(const ChanArgs& a, hipStream_t s, hipError_t* err) {
 }  // namespace sdsp
 
 // tools/chan_ab.py encoding: 1 no FFT, 2 no loads, 4 no stores, 8 plain stores,
-// 16 nontemporal loads, 32 / 64 odd workgroups start ~6.8 / ~3.4 us late
+// 16 nontemporal loads, 32 / 64 odd workgroups start ~6.8 / ~3.4 us late; bits from 128 up
+// pass through as the kernel's LAB bits (128 write-through stores, 256 nontemporal round loads)
 extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablation(int v) {
-    sdsp::g_chan_lab = (v & 7) | ((v >> 2) & 24) | ((v & 8) ? 32 : 0) | ((v & 16) ? 64 : 0);
+    sdsp::g_chan_lab = (v & 7) | ((v >> 2) & 24) | ((v & 8) ? 32 : 0) | ((v & 16) ? 64 : 0) | (v & ~127);
 }
+
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_fft_policy(int v) { sdsp::g_fft_policy = v & 3; }
