@@ -12,10 +12,13 @@
 namespace sdsp {
 
 static int g_chan_lab = 0;
-static int g_fft_policy = 0;  // 4-step L = 1024 passes: bit 0 nontemporal loads, bit 1 nontemporal stores
+static int g_fft_policy = 0;  // 4-step L = 1024 passes: bit 0 nontemporal loads, bit 1 nontemporal stores,
+                              // bit 2 no inter-pass twiddle (ablation)
 
-bool try_launch_fft1024_pass(const FftPass& p, hipStream_t s, hipError_t* err) {
-    switch (g_fft_policy) {
+bool try_launch_fft1024_pass(const FftPass& p_, hipStream_t s, hipError_t* err) {
+    FftPass p = p_;
+    if (g_fft_policy & 4) p.Ntw = 0;  // ablation: the column pass without its inter-pass twiddle (wrong results)
+    switch (g_fft_policy & 3) {
         case 1: return try_launch_fft1024_pass_t<2, 0>(p, s, err);
         case 2: return try_launch_fft1024_pass_t<0, 2>(p, s, err);
         case 3: return try_launch_fft1024_pass_t<2, 2>(p, s, err);
@@ -47,4 +50,4 @@ extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablatio
     sdsp::g_chan_lab = (v & 7) | ((v >> 2) & 24) | ((v & 8) ? 32 : 0) | ((v & 16) ? 64 : 0) | (v & ~127);
 }
 
-extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_fft_policy(int v) { sdsp::g_fft_policy = v & 3; }
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_fft_policy(int v) { sdsp::g_fft_policy = v & 7; }
