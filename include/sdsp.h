@@ -144,8 +144,10 @@ typedef enum {
                                      as 3 with eight / four frames per round (waves 0..7 / 0..3 transform);
                                      0 = per-frame kernel */
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
-    SDSP_TUNE_OLS_KERNEL = 14,   /* overlap-save interior segments (16-byte aligned rows): 0 (default) one-shot
-                                    XCD-ordered kernel, 1 persistent packed kernel (L <= 1025), 2 scalar kernel */
+    SDSP_TUNE_OLS_KERNEL = 14,   /* overlap-save segments (16-byte aligned rows): 0 (default) one-shot
+                                    XCD-ordered kernel for every segment (it also writes the next history),
+                                    1 persistent packed kernel for the interior segments (L <= 1025),
+                                    2 scalar kernel, 3 the one-shot kernel with 16-byte lanes */
     SDSP_TUNE_CHAN_XCD_ORDER = 15, /* streaming channeliser: 1 (default) = each XCD walks a contiguous
                                      eighth of the frame chunks, 0 = launch order */
     SDSP_TUNE_HOST_STEP = 16,     /* FIR / decimator: 1 (default) = execute(sample), push and host blocks with

@@ -330,22 +330,32 @@ void ols_interior_range(long long n, int h2, long long* lo, long long* hi) {
     *hi = b;
 }
 
-// Kernel choice (OlsPlan::kernel, SDSP_TUNE_OLS_KERNEL): with 16-byte rows the
-// interior segments run in the one-shot kernel (default) or the persistent packed
-// kernel (h2 <= 4), the boundary segments in fir_ols4096_edge_kernel; otherwise
+// Kernel choice (OlsPlan::kernel, SDSP_TUNE_OLS_KERNEL): with 16-byte rows every
+// segment runs in the one-shot kernel (default; it also writes the next history), or
+// the interior segments in the persistent packed kernel (h2 <= 4) and the boundary
+// segments in fir_ols4096_edge_kernel; otherwise
 // everything runs in the scalar persistent kernel.  All choices compute the same
 // transform (rounding differs only in the one-shot kernel's twiddle products).
-hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
-                          size_t channels, int num_cus, hipStream_t s) {
+hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
+                          int L, size_t channels, int num_cus, hipStream_t s, bool* hist_done) {
+    *hist_done = false;
     if (n == 0) return hipSuccess;
     const int h2 = p.halo_rows;
     const long long V = 4096 - 256 * h2;
     const long long nseg = ((long long)n + V - 1) / V;
     const bool rows16 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0 &&
                         (channels == 1 || n % 2 == 0);
-    const bool os = p.kernel == kOlsOneShot;
+    const bool os = p.kernel == kOlsOneShot || p.kernel == kOlsOneShotWide;
     const bool pk = p.kernel == kOlsPersistent && h2 <= 4;
-    if (rows16 && (os || pk)) {
+    if (rows16 && os) {
+        // one grid: boundary segments, interior segments and (n >= L - 1) the history update
+        const bool fused_hist = n >= (size_t)(L - 1);
+        hipError_t e = launch_fir_ols_os(p, x, hist, fused_hist ? new_hist : nullptr, y, n, L - 1, channels, s,
+                                         p.kernel == kOlsOneShotWide);
+        if (e == hipSuccess) *hist_done = fused_hist;
+        return e;
+    }
+    if (rows16 && pk) {
         long long lo, hi;
         ols_interior_range((long long)n, h2, &lo, &hi);
         const long long nedge = lo + (nseg - hi);
@@ -356,8 +366,7 @@ hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, voi
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
-        return os ? launch_fir_ols_os(p, x, y, n, channels, s, lo, hi)
-                  : launch_fir_ols_pk(p, x, y, n, channels, s, lo, hi);
+        return launch_fir_ols_pk(p, x, y, n, channels, s, lo, hi);
     }
     long long blocks = (long long)num_cus * 2;
     if (blocks > nseg) blocks = nseg;

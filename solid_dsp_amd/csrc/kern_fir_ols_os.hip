@@ -67,6 +67,7 @@ template <bool WAVE> __device__ __forceinline__ void phase_sync() {
 }
 
 typedef unsigned int u2v __attribute__((ext_vector_type(2)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
 constexpr int kBufWord3 = 0x00020000;  // raw buffer descriptor word 3 (gfx9 family)
 
 // x = D_{k>>2} C_{k&3} for C_b = c[b-1], D_a = d[a-1] (k = 0 -> 1)
@@ -75,6 +76,29 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
     if (a == 0) return b == 0 ? f2{1.0f, 0.0f} : c[b - 1];
     if (b == 0) return d[a - 1];
     return pmul(d[a - 1], c[b - 1]);
+}
+
+// lane pair (2c, 2c + 1) exchange: even lanes lo = a, odd lanes lo = the partner's b; odd lanes
+// hi = b, even lanes hi = the partner's a.  Loads: (a, b) = columns (2c, 2c + 1) of row k + 8h ->
+// (lo, hi) = rows (k, 8 + k) of column 2c + h.  Stores: (a, b) = rows (k, 8 + k) of column 2c + h
+// -> (lo, hi) = columns (2c, 2c + 1) of row k + 8h.  One v_cndmask_b32 with a quad_perm DPP
+// operand per dword (the partner's register read in the same instruction); the s_nop covers
+// the DPP read-after-VALU-write hazard of an operand the compiler computed just before.
+[[maybe_unused]] __device__ __forceinline__ void pair_exchange(f2 a, f2 b, f2& lo, f2& hi) {
+    float l0, l1, h0, h1;
+    asm("s_nop 1\n\t"
+        "s_mov_b32 vcc_lo, 0x55555555\n\t"
+        "s_mov_b32 vcc_hi, 0x55555555\n\t"
+        "v_cndmask_b32_dpp %0, %6, %4, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %1, %7, %5, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_not_b64 vcc, vcc\n\t"
+        "v_cndmask_b32_dpp %2, %4, %6, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_dpp %3, %5, %7, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+        : "=&v"(l0), "=&v"(l1), "=&v"(h0), "=&v"(h1)
+        : "v"(a.x), "v"(a.y), "v"(b.x), "v"(b.y)
+        : "vcc");
+    lo = f2{l0, l1};
+    hi = f2{h0, h1};
 }
 
 }  // namespace
@@ -91,31 +115,79 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores; 16384
 // plain (not nontemporal) input loads; 32768 all six twiddle bases loaded (the round-3 form;
 // 49152 = the round-3 kernel); 131072 with 4: the HBM-only pattern in 16-byte lanes (the NCO
-// kernel's shape).
+// kernel's shape); 262144 clock stamps (lab builds that define SDSP_OLS_STAMPS only: every 32nd
+// workgroup records s_memtime / s_memrealtime at entry and exit into g_ols_stamps, a buffer no
+// other code reads; the in-kernel clock of MI355X_MICROARCH.md "DVFS give-back" item 6).
 template <int ABL>
-__device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const float4* __restrict__ Hs,
+__device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f2* __restrict__ hist,
+                                               f2* __restrict__ new_hist, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
-                                               int h2, f2* img, int t) {
+                                               long long n, int Lm1, int h2, f2* img, int t) {
     const int hi4 = t >> 4, lo4 = t & 15;
-    const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, 32768, kBufWord3);
-    const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, 32768, kBufWord3);
+    // the segment's window x[base, base + 4096) as a raw buffer: past the end of the stream
+    // (the last segment) loads return 0 and stores are dropped, so only a window that starts
+    // before the stream (base < 0: the first segments) needs the history path below
+    const long long rem = n - base;
+    const int nrec = rem >= 4096 ? 32768 : (int)(8 * rem);
+    const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, nrec, kBufWord3);
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, nrec, kBufWord3);
     const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
     const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0, 2048 * 16, kBufWord3);
+    constexpr int kLdAux = (ABL & 16384) ? 0 : 2;  // nontemporal (aux 2)
+    // twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build), requested
+    // before the segment's rows (L2 hits that land while the rows stream in)
+    auto tab = [&](int lane, int off) {
+        if constexpr ((ABL & 4096) != 0) {
+            const float u = 1e-3f * (float)lane + 1e-6f * (float)off;
+            return float4{u, 0.5f - u, 0.25f + u, 1.0f - u};
+        } else {
+            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lane, off, 0));
+        }
+    };
+    float4 tq[6];  // the raw table loads (products formed once the rows are requested)
+    if constexpr ((ABL & (32768 | 4096)) == 0) {
+        tq[0] = tab(t, 16 * kOlsOsTabCD), tq[1] = tab(lo4, 16 * kOlsOsTabEF);
+    } else {
+        tq[0] = tab(t, 0), tq[1] = tab(t, 4096), tq[2] = tab(t, 8192);
+        tq[3] = tab(lo4, 12288), tq[4] = tab(lo4, 12544), tq[5] = tab(lo4, 12800);
+    }
     f2 v[16];
+    if (base < 0) {
+        // rows before the stream come from the handle's history (the last Lm1 inputs, oldest
+        // first); positions before the history read as 0 (an out-of-range offset)
+        const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)hist, (short)0, 8 * Lm1, kBufWord3);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int r = (ABL & 256) ? 15 - i : i;
-        if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
-        else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
-        else if constexpr ((ABL & 16384) != 0)
-            v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
-        else  // nontemporal (aux 2)
-            v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 2));
+        for (int r = 0; r < 16; ++r) {
+            const long long pos = base + 256 * r;
+            if (pos >= 0) {
+                v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+            } else {
+                const long long e = Lm1 + pos + t;
+                v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rp, e >= 0 ? (int)(8 * e) : 0x7ffffff0, 0, 0));
+            }
+        }
+    } else if constexpr ((ABL & 524288) != 0) {
+        // 16-byte lanes: lane t = 2c + h loads columns (2c, 2c + 1) of rows k + 8h, then one DPP
+        // exchange per dword with its partner lane t ^ 1 gives it column t over the 16 rows
+        f4v q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            q[k] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, 16 * (t >> 1) + 16384 * (t & 1),
+                                                                                2048 * k, kLdAux));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pair_exchange(f2{q[k].x, q[k].y}, f2{q[k].z, q[k].w}, v[k], v[8 + k]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int r = (ABL & 256) ? 15 - i : i;
+            if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
+            else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
+            else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, kLdAux));
+        }
     }
     if constexpr ((ABL & 4) && (ABL & 131072)) {
         // HBM-only with the NCO kernel's lane shape: the segment as eight 4 KB rows of 16-byte
         // lanes (lane t: bytes 16 t + 4096 k), the halo's bytes not stored
-        typedef unsigned u4v __attribute__((ext_vector_type(4)));
         u4v w[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) w[k] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(rx, 16 * t, 4096 * k, 2));
@@ -139,22 +211,13 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         }
         return;
     }
-    // twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build)
-    auto tab = [&](int lane, int off) {
-        if constexpr ((ABL & 4096) != 0) {
-            const float u = 1e-3f * (float)lane + 1e-6f * (float)off;
-            return float4{u, 0.5f - u, 0.25f + u, 1.0f - u};
-        } else {
-            return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lane, off, 0));
-        }
-    };
     f2 Cb[3], Da[3], Eb[3], Fa[3];
     if constexpr ((ABL & (32768 | 4096)) == 0) {
         // the first power of each base from L2 ({C1, D1} per column, {E1, F1} per row: two
         // 16-byte loads where the six-base form takes six), the others as products (W^2 = W W,
         // W^3 = W^2 W): a third of the table traffic per segment, results within rounding of the
         // six-base form (rel-RMS 2.2e-7 between the two on cfg2)
-        const float4 cd = tab(t, 16 * kOlsOsTabCD), ef = tab(lo4, 16 * kOlsOsTabEF);
+        const float4 cd = tq[0], ef = tq[1];
         const f2 c1 = f2{cd.x, cd.y}, d1 = f2{cd.z, cd.w}, e1 = f2{ef.x, ef.y}, f1 = f2{ef.z, ef.w};
         const f2 c2 = pmul(c1, c1), d2 = pmul(d1, d1), e2 = pmul(e1, e1), f2_ = pmul(f1, f1);
         Cb[0] = c1, Cb[1] = c2, Cb[2] = pmul(c2, c1);
@@ -162,12 +225,21 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         Eb[0] = e1, Eb[1] = e2, Eb[2] = pmul(e2, e1);
         Fa[0] = f1, Fa[1] = f2_, Fa[2] = pmul(f2_, f1);
     } else {
-        const float4 b0 = tab(t, 0), b1 = tab(t, 4096), b2 = tab(t, 8192);
-        const float4 e0 = tab(lo4, 12288), e1 = tab(lo4, 12544), e2 = tab(lo4, 12800);
+        const float4 b0 = tq[0], b1 = tq[1], b2 = tq[2], e0 = tq[3], e1 = tq[4], e2 = tq[5];
         Cb[0] = f2{b0.x, b0.y}, Cb[1] = f2{b0.z, b0.w}, Cb[2] = f2{b1.x, b1.y};
         Da[0] = f2{b1.z, b1.w}, Da[1] = f2{b2.x, b2.y}, Da[2] = f2{b2.z, b2.w};
         Eb[0] = f2{e0.x, e0.y}, Eb[1] = f2{e0.z, e0.w}, Eb[2] = f2{e1.x, e1.y};
         Fa[0] = f2{e1.z, e1.w}, Fa[1] = f2{e2.x, e2.y}, Fa[2] = f2{e2.z, e2.w};
+    }
+    if (new_hist != nullptr) {
+        // the call's last segment: its window holds the last Lm1 inputs (halo >= Lm1), which
+        // become the history of the next call (ping-pong buffer: never the one read above)
+        const long long h0 = n - Lm1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const long long i = base + 256 * r + t - h0;
+            if (i >= 0 && i < Lm1) new_hist[i] = v[r];
+        }
     }
     f2* col = img + t + (t >> 4);  // (r, t) at col[r * kRow]
 
@@ -235,47 +307,87 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         if (acc.x == 1.2345e30f) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, acc), ry, 8 * t, 0, 0);
         return;
     }
-    // nontemporal stores (3.14 -> 3.08 ms on cfg2, in-process A/B)
+    // nontemporal stores (3.14 -> 3.08 ms on cfg2, in-process A/B); rows < h2 wrap and are dropped,
+    // positions past the stream fall outside the descriptor (dropped)
     constexpr int kStAux = (ABL & 8192) ? 16 : (ABL & 128) ? 0 : 2;  // 16: write-through (sc1), lab
+    if constexpr ((ABL & 524288) != 0) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int r = (ABL & 512) ? 15 - i : i;
-        if (r >= h2)
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, kStAux);
+        for (int k = 0; k < 8; ++k) {
+            f2 a, b;
+            pair_exchange(v[kout(k)], v[kout(8 + k)], a, b);
+            if (k + 8 * (t & 1) >= h2)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, f4v{a.x, a.y, b.x, b.y}), ry,
+                                                       16 * (t >> 1) + 16384 * (t & 1), 2048 * k, kStAux);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int r = (ABL & 512) ? 15 - i : i;
+            if (r >= h2)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, v[kout(r)]), ry, 8 * t, 2048 * r, kStAux);
+        }
     }
 }
 
+#ifdef SDSP_OLS_STAMPS
+__device__ unsigned long long g_ols_stamps[4 * 8192];
+#endif
+
 template <int ABL>
 __global__ void __launch_bounds__(256, 4)
-fir_ols_os_kernel(const f2* __restrict__ x, const float4* __restrict__ Hs, const float4* __restrict__ tb,
-                  f2* __restrict__ y, long long n, long long lo, long long hi, long long q, int h2) {
+fir_ols_os_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, f2* __restrict__ new_hist,
+                  const float4* __restrict__ Hs, const float4* __restrict__ tb, f2* __restrict__ y, long long n,
+                  long long nseg, long long q, int h2, int Lm1) {
     __shared__ __attribute__((aligned(16))) f2 img[16 * kRow];
     const int xc = blockIdx.x & 7;
     long long j = blockIdx.x >> 3;
     if constexpr ((ABL & 1024) != 0) j = j < (q + 1) / 2 ? 2 * j : 2 * (j - (q + 1) / 2) + 1;
-    const long long seg = lo + (long long)xc * q + j;
-    const long long xe = lo + (long long)(xc + 1) * q;
-    if (seg >= (xe < hi ? xe : hi)) return;  // uniform over the workgroup
+    const long long seg = (long long)xc * q + j;
+    const long long xe = (long long)(xc + 1) * q;
+    if (seg >= (xe < nseg ? xe : nseg)) return;  // uniform over the workgroup
     const int V = 4096 - 256 * h2;
-    ols_os_segment<ABL>(x, Hs, tb, y, (long long)blockIdx.y * n + seg * V - 256 * h2, h2, img, threadIdx.x);
+    const long long ch = blockIdx.y;
+#ifdef SDSP_OLS_STAMPS
+    unsigned long long m0 = 0, r0 = 0;
+    if constexpr ((ABL & 262144) != 0) m0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    ols_os_segment<ABL>(x + ch * n, hist + ch * Lm1,
+                        (new_hist != nullptr && seg == nseg - 1) ? new_hist + ch * Lm1 : nullptr, Hs, tb, y + ch * n,
+                        seg * V - 256 * h2, n, Lm1, h2, img, threadIdx.x);
+#ifdef SDSP_OLS_STAMPS
+    if constexpr ((ABL & 262144) != 0) {
+        const unsigned long long m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0 && (blockIdx.x & 31) == 0) {
+            unsigned long long* o = g_ols_stamps + 4 * ((blockIdx.x >> 5) & 8191);
+            o[0] = m0, o[1] = r0, o[2] = m1, o[3] = r1;
+        }
+    }
+#endif
 }
 
-// interior segments [lo, hi) of every channel; ABL as above (0 = the product kernel)
+// every segment of every channel in one grid (the first segments read the history, the last
+// one is bounded by the stream and, with new_hist, writes the next call's history); ABL as
+// above (0 = the product kernel)
 template <int ABL>
-hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
-                               long long lo, long long hi, size_t dyn_lds) {
-    if (hi <= lo) return hipSuccess;
-    if (p.halo_rows < 1 || p.halo_rows > 15) return hipErrorInvalidValue;
-    const long long q = (hi - lo + 7) / 8;
+hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
+                               int Lm1, size_t channels, hipStream_t s, size_t dyn_lds) {
+    if (n == 0) return hipSuccess;
+    const int h2 = p.halo_rows;
+    if (h2 < 1 || h2 > 15 || Lm1 > 256 * h2) return hipErrorInvalidValue;
+    const long long V = 4096 - 256 * h2;
+    const long long nseg = ((long long)n + V - 1) / V;
+    const long long q = (nseg + 7) / 8;
     const dim3 grid((unsigned)(8 * q), (unsigned)channels);
-    hipLaunchKernelGGL(fir_ols_os_kernel<ABL>, grid, dim3(256), dyn_lds, s, (const f2*)x, (const float4*)p.d_pkt,
-                       (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, p.halo_rows);
+    hipLaunchKernelGGL(fir_ols_os_kernel<ABL>, grid, dim3(256), dyn_lds, s, (const f2*)x, (const f2*)hist,
+                       (f2*)new_hist, (const float4*)p.d_pkt, (const float4*)p.d_ostab, (f2*)y, (long long)n, nseg, q,
+                       h2, Lm1);
     return hipGetLastError();
 }
 
-hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
-                             long long lo, long long hi) {
-    return launch_fir_ols_os_t<0>(p, x, y, n, channels, s, lo, hi, 0);
+hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
+                             int Lm1, size_t channels, hipStream_t s, bool wide) {
+    return wide ? launch_fir_ols_os_t<524288>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0)
+                : launch_fir_ols_os_t<0>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0);
 }
 
 }  // namespace sdsp

@@ -573,7 +573,7 @@ int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     switch (key) {
         case SDSP_TUNE_OLS_KERNEL:  // every value computes the full output (performance only)
-            if (value < kOlsOneShot || value > kOlsScalar) return SDSP_E_INVALID_ARGUMENT;
+            if (value < kOlsOneShot || value > kOlsOneShotWide) return SDSP_E_INVALID_ARGUMENT;
             h->ols_kernel = value;
             h->ols.kernel = value;
             return SDSP_OK;
@@ -677,6 +677,7 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
     // work queued on another stream (the fence) reads or writes the history this launch uses
     SDSP_TRY(h->fence.order_before(s), "order after queued work");
     const void* hist = h->d_hist[h->cur].p;
+    bool hist_done = false;  // the overlap-save launch wrote the next history itself
     if (h->M == 1) {
         const int algo = fir_resolve_algo(h, n);
         if (algo == SDSP_ALGO_FFT) {
@@ -684,7 +685,9 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
                 int st = ols_build(h);
                 if (st) return st;
             }
-            SDSP_TRY(launch_fir_ols(h->ols, d_in, hist, d_out, n, (int)h->L, h->channels, h->cus, s), "fir ols");
+            SDSP_TRY(launch_fir_ols(h->ols, d_in, hist, h->d_hist[h->cur ^ 1].p, d_out, n, (int)h->L, h->channels,
+                                    h->cus, s, &hist_done),
+                     "fir ols");
         } else {
             FirArgs a{d_in, hist, h->d_taps_rev.p, h->scale.data(), d_out, n, n, h->channels, (int)h->L, 1, 0,
                       algo != SDSP_ALGO_FMA};
@@ -699,8 +702,9 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
         SDSP_TRY(launch_decim_direct(h->dtype, a, s), "decim direct");
         h->ci = (h->ci + n) % h->M;
     }
-    SDSP_TRY(launch_hist_update(h->dtype, d_in, hist, h->d_hist[h->cur ^ 1].p, n, (int)h->L - 1, h->channels, s),
-             "history update");
+    if (!hist_done)
+        SDSP_TRY(launch_hist_update(h->dtype, d_in, hist, h->d_hist[h->cur ^ 1].p, n, (int)h->L - 1, h->channels, s),
+                 "history update");
     h->cur ^= 1;
     SDSP_TRY(h->fence.record(s), "record fence");
     return SDSP_OK;

@@ -160,10 +160,13 @@ struct StreamFence {
         return hipStreamWaitEvent(s, ev[cur], 0);
     }
     static bool legacy(hipStream_t s) { return s == nullptr || s == hipStreamLegacy; }
+    // the marker stays pending until a synchronize has succeeded (a failed wait must
+    // not let later host operations skip it)
     hipError_t wait() {
         if (!pending) return hipSuccess;
-        pending = false;
-        return hipEventSynchronize(ev[cur]);
+        const hipError_t e = hipEventSynchronize(ev[cur]);
+        if (e == hipSuccess) pending = false;
+        return e;
     }
 };
 

@@ -31,6 +31,7 @@ hipError_t launch_hist_update(int dtype, const void* x, const void* old_hist, vo
 constexpr int kOlsOneShot = 0;     // interior segments: one-shot XCD-ordered kernel (kern_fir_ols_os.hip)
 constexpr int kOlsPersistent = 1;  // persistent packed kernel, kOlsSegsPerBlock segments per workgroup
 constexpr int kOlsScalar = 2;      // scalar persistent kernel for every segment (kern_fir_ols.hip)
+constexpr int kOlsOneShotWide = 3;  // the one-shot kernel with 16-byte lanes (pair exchange by DPP)
 constexpr int kOlsSegsPerBlock = 16;
 // W4096 column bases [3][256], W256 row bases [3][16], then the first powers alone: {C1, D1}
 // per column [256] and {E1, F1} per row [16] (kern_fir_ols_os.hip, runtime.cpp ols_build)
@@ -49,13 +50,15 @@ struct OlsPlan {
                               // (C1 C2 | C3 D1 | D2 D3), then [16][8] float4 W256 rows
 };
 constexpr int kOlsN = 4096;
-hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* y, size_t n, int L,
-                          size_t channels, int num_cus, hipStream_t s);
+// new_hist: the next call's history buffer.  *hist_done = true when the launch also wrote it
+// (the one-shot kernel does, for n >= L - 1); otherwise the caller runs the history update.
+hipError_t launch_fir_ols(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
+                          int L, size_t channels, int num_cus, hipStream_t s, bool* hist_done);
 // interior segments [lo, hi) of a call: whole input window and all outputs inside the stream
 void ols_interior_range(long long n, int h2, long long* lo, long long* hi);
 // interior-segment kernels (16-byte rows)
-hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
-                             long long lo, long long hi);
+hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
+                             int Lm1, size_t channels, hipStream_t s, bool wide);
 hipError_t launch_fir_ols_pk(const OlsPlan& p, const void* x, void* y, size_t n, size_t channels, hipStream_t s,
                              long long lo, long long hi);
 

@@ -240,9 +240,13 @@ class SecondOrderFilter:
 
     @classmethod
     def new(cls, feed_forward, feed_back, coef_dtype=np.float64, sample_dtype=np.float64, **kw):  # sos.rs:55-75
-        """SecondOrderFilter::<f64, f64>::new -- the only instantiation the reference's bounds admit"""
+        """SecondOrderFilter::<f64, f64>::new.  The reference is generic
+        (`impl<C: Copy + Num + Sum, T: Copy> SecondOrderFilter<C, T>`, sos.rs:41), so other
+        instantiations such as <f32, f32> compile there; this binding offers f64 only, and
+        f32 / complex-sample SecondOrderFilter parity is not covered."""
         if np.dtype(coef_dtype) != np.float64 or np.dtype(sample_dtype) != np.float64:
-            raise TypeError("SecondOrderFilter is SecondOrderFilter<f64, f64>")
+            raise NotImplementedError("this binding implements SecondOrderFilter<f64, f64> only "
+                                      "(the reference's generic instantiations are not bound)")
         return cls(feed_forward, feed_back, **kw)
 
     def execute(self, sample: float) -> float:  # sos.rs:92-114 (Left(input))

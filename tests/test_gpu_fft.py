@@ -131,6 +131,8 @@ def test_channelizer_1024_streaming_variants(variant, fpb, K, xcd):
         O.lib().orc_channelize(O._ptr(h.astype(np.float64)), len(h), M, O._ptr(x[s].astype(np.complex128)),
                                M * frames, O._ptr(ref))
         assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-6
+        # §8d max-abs bound, as in test_channelizer_vs_restatement
+        assert np.abs(y[s] - ref.reshape(frames, M)).max() <= 1e-6 * np.abs(h).sum() * np.abs(x[s]).max() * np.sqrt(M)
 
 
 @pytest.mark.parametrize("variant,fpb", [(1, 16), (2, 8), (3, 16), (4, 8), (5, 8), (6, 8)])
@@ -153,6 +155,8 @@ def test_channelizer_1024_persistent_chunk_walk(variant, fpb, xcd):
         O.lib().orc_channelize(O._ptr(h.astype(np.float64)), len(h), M, O._ptr(x[s].astype(np.complex128)),
                                M * frames, O._ptr(ref))
         assert rel_rms(y[s], ref.reshape(frames, M)) <= 1e-6
+        # §8d max-abs bound, as in test_channelizer_vs_restatement
+        assert np.abs(y[s] - ref.reshape(frames, M)).max() <= 1e-6 * np.abs(h).sum() * np.abs(x[s]).max() * np.sqrt(M)
 
 
 @pytest.mark.parametrize("cdt,sdt,kind", [(np.float64, np.float64, 0), (np.float64, np.complex128, 1),

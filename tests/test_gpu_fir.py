@@ -144,23 +144,30 @@ def test_fir_fft_tolerance(dt, cdt, L):
     assert np.abs(y - ref).max() <= bound
 
 
-OLS_ONESHOT, OLS_PERSISTENT, OLS_SCALAR = 0, 1, 2
+OLS_ONESHOT, OLS_PERSISTENT, OLS_SCALAR, OLS_ONESHOT_WIDE = 0, 1, 2, 3
 TUNE_OLS_KERNEL = 14
 
 
 @pytest.mark.parametrize("L", [2, 64, 256, 257, 700, 1025, 2000, 3841])
 @pytest.mark.parametrize("ch", [1, 2, 3])
-def test_fir_fft_oneshot_kernel_tolerance(L, ch):
-    # default interior kernel (one-shot, XCD-ordered) + boundary kernel, ragged calls that
-    # cover all-boundary calls (n < one window), history carry and both edges, every halo
-    # size h2 = 1..15; ch = 3 with odd n falls back to the scalar kernel (8-byte rows)
+@pytest.mark.parametrize("kern", [OLS_ONESHOT, OLS_ONESHOT_WIDE])
+def test_fir_fft_oneshot_kernel_tolerance(L, ch, kern):
+    # default kernel (one-shot, XCD-ordered, every segment of the call in one grid: the first
+    # segments read the history, the last one is bounded by the stream and writes the next
+    # history), ragged calls that cover single-segment calls (n < one window), calls shorter
+    # than the history (n = 1: the separate history update), history carry and both edges,
+    # every halo size h2 = 1..15; ch = 3 with odd n falls back to the scalar kernel (8-byte
+    # rows).  kern = 3: the same kernel with 16-byte lanes
     h = _f32_taps(L, 0.1)
     h = (h * np.exp(2j * np.pi * 0.05 * np.arange(L))).astype(C64)
     x = O.synth(20250229, 6, 0, 300000 * ch, complex_=True).reshape(ch, -1) if ch > 1 else \
         O.synth(20250229, 6, 0, 300000, complex_=True)
     f = FIRFilter(h, C64(0.2), sample_dtype=C64, channels=ch, algo=sd.ALGO_FFT)
-    cuts = [0, 1, 3000, 7001, 70002, 207714, 300000]
+    assert sd.lib().sdsp_fir_set_tuning(f._h, TUNE_OLS_KERNEL, kern) == 0
+    cuts = [0, 1, 3000, 7001, 70002, 207714, 207715, 300000]
     y = np.concatenate([f.execute_block(x[..., a:b]) for a, b in zip(cuts[:-1], cuts[1:])], axis=-1)
+    hist, _ = f.get_state()
+    assert bits_equal(hist, x[..., -(L - 1):].reshape(-1))
     for c in range(ch):
         xc = x[c] if ch > 1 else x
         yc = y[c] if ch > 1 else y
@@ -194,8 +201,8 @@ def test_fir_tuning_rejects_retired_and_bad_keys():
     f = FIRFilter(_f32_taps(64, 0.1), F32(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
     for key in (1, 2, 3, 4, 5, 10, 11, 12, 13, 99):
         assert sd.lib().sdsp_fir_set_tuning(f._h, key, 1) == 90, key
-    assert sd.lib().sdsp_fir_set_tuning(f._h, TUNE_OLS_KERNEL, 3) == 90
-    for v in (OLS_ONESHOT, OLS_PERSISTENT, OLS_SCALAR):
+    assert sd.lib().sdsp_fir_set_tuning(f._h, TUNE_OLS_KERNEL, 4) == 90
+    for v in (OLS_ONESHOT, OLS_PERSISTENT, OLS_SCALAR, OLS_ONESHOT_WIDE):
         assert sd.lib().sdsp_fir_set_tuning(f._h, TUNE_OLS_KERNEL, v) == 0
 
 
@@ -772,6 +779,10 @@ def test_time_sharded_stream_on_device(algo, M):
     assert len(got) == len(full)
     if algo == "exact":
         assert bits_equal(got, full)
+        # and against the f32 restatement of the whole stream (the reference order
+        # at the handle's precision), not only the device's own single stream
+        ref32 = (O.fir(O.RC32, h, s) if M == 1 else O.decim(O.RC32, h, s, M)).execute_block(x)
+        assert bits_equal(got, ref32)
     else:
         # the fast kernels' time-sharded stream against the f64 restatement of the
         # whole stream, both §8d criteria

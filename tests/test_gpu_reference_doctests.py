@@ -42,155 +42,175 @@ def _round(v):  # f64::round: half away from zero
     return math.floor(v + 0.5) if v >= 0 else -math.floor(-v + 0.5)
 
 
-def test_filter_fir_mod_l73():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l73(host_step):
     """src/filter/fir/mod.rs:73"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
 
 
-def test_filter_fir_mod_l96():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l96(host_step):
     """src/filter/fir/mod.rs:96"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     filter.set_scale(2.0)
     _eq(filter.get_scale(), 2.0)
 
 
-def test_filter_fir_mod_l116():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l116(host_step):
     """src/filter/fir/mod.rs:116"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     _eq(filter.get_scale(), 1.0)
 
 
-def test_filter_fir_mod_l132():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l132(host_step):
     """src/filter/fir/mod.rs:132"""
     coefs = [0.0] * 12
-    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     len = _len(filter)
     _eq(len, 12)
 
 
-def test_filter_fir_mod_l150():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l150(host_step):
     """src/filter/fir/mod.rs:150"""
     coefs = [0.0] * 12
-    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     _eq(filter.is_empty(), False)
 
 
-def test_filter_fir_mod_l166():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l166(host_step):
     """src/filter/fir/mod.rs:166"""
     coefs = [0.0] * 12
-    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     ref_coefs = filter.coefficients()
     _eq(coefs, ref_coefs)
 
 
-def test_filter_fir_mod_l195():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l195(host_step):
     """src/filter/fir/mod.rs:195"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     window = [complex(2.02, 0.0), complex(4.04, 0.0), complex(1.02, 0.0), complex(0.23, 0.0), complex(9.19, 0.0)]
     output = filter.execute(window[0])
     _eq(output[0], complex(10.1, 0.0))
 
 
-def test_filter_fir_mod_l221():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l221(host_step):
     """src/filter/fir/mod.rs:221"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = FIRFilter.new(coefficients, 1.0, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     window = [complex(2.02, 0.0), complex(4.04, 0.0), complex(1.02, 0.0), complex(0.23, 0.0), complex(9.19, 0.0)]
     output = filter.execute_block(window)
     _eq(output[4], complex(60.03, 0.0))
 
 
-def test_filter_fir_mod_l247():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l247(host_step):
     """src/filter/fir/mod.rs:247"""
     coefs = firdes_notch(25, 0.35, 120.0)
-    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.float64)
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.float64, host_step=host_step)
     response = filter.frequency_response(0.0)
     _eq(_round(response.real), 1.0)
     _eq(response.imag, 0.0)
 
 
-def test_filter_fir_mod_l279():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_mod_l279(host_step):
     """src/filter/fir/mod.rs:279"""
     coefs = firdes.firdes_notch(12, 0.35, 120.0)
-    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.float64)
+    filter = FIRFilter.new(coefs, 1.0, coef_dtype=np.float64, sample_dtype=np.float64, host_step=host_step)
     delay = filter.group_delay(0.0)
     _eq(int(delay + 0.5), 12)
 
 
-def test_filter_fir_decim_l21():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l21(host_step):
     """src/filter/fir/decim.rs:21"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
 
 
-def test_filter_fir_decim_l50():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l50(host_step):
     """src/filter/fir/decim.rs:50"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     filter.set_scale(2.0)
     _eq(filter.get_scale(), 2.0)
 
 
-def test_filter_fir_decim_l70():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l70(host_step):
     """src/filter/fir/decim.rs:70"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     _eq(filter.get_scale(), 1.0)
 
 
-def test_filter_fir_decim_l88():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l88(host_step):
     """src/filter/fir/decim.rs:88"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     _eq(filter.get_decimation(), 2)
 
 
-def test_filter_fir_decim_l106():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l106(host_step):
     """src/filter/fir/decim.rs:106"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     filter.push(complex(4.0, 0.0))
 
 
-def test_filter_fir_decim_l126():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l126(host_step):
     """src/filter/fir/decim.rs:126"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     window = [complex(2.02, 0.0), complex(4.04, 0.0)]
     filter.write(window)
 
 
-def test_filter_fir_decim_l145():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l145(host_step):
     """src/filter/fir/decim.rs:145"""
     coefs = [0.0] * 12
-    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     len = _len(filter)
     _eq(len, 12)
 
 
-def test_filter_fir_decim_l163():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l163(host_step):
     """src/filter/fir/decim.rs:163"""
     coefs = [0.0] * 12
-    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     _eq(filter.is_empty(), False)
 
 
-def test_filter_fir_decim_l179():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l179(host_step):
     """src/filter/fir/decim.rs:179"""
     coefs = [0.0] * 12
-    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefs, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     ref_coefs = filter.coefficients()
     _eq(coefs, ref_coefs)
 
 
-def test_filter_fir_decim_l208():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l208(host_step):
     """src/filter/fir/decim.rs:208"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     window = [complex(2.02, 0.0), complex(4.04, 0.0)]
     first_output = filter.execute(window[0])
     second_output = filter.execute(window[1])
@@ -198,10 +218,11 @@ def test_filter_fir_decim_l208():
     _eq(second_output, [complex(28.28, 0.0)])
 
 
-def test_filter_fir_decim_l237():
+@pytest.mark.parametrize("host_step", [None, False])
+def test_filter_fir_decim_l237(host_step):
     """src/filter/fir/decim.rs:237"""
     coefficients = [1.0, 2.0, 3.0, 4.0, 5.0]
-    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128)
+    filter = DecimatingFIRFilter.new(coefficients, 1.0, 2, coef_dtype=np.float64, sample_dtype=np.complex128, host_step=host_step)
     window = [complex(2.02, 0.0), complex(4.04, 0.0), complex(1.02, 0.0), complex(0.23, 0.0)]
     output = filter.execute_block(window)
     _eq(output, [complex(28.28, 0.0), complex(21.39, 0.0)])

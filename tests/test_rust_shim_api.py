@@ -1,6 +1,6 @@
 """The Rust shim (rust/solid-sdsp, §8f row 1) declares the reference's public API
 of the hot path exactly: for every file of src/filter/{fir,iir}/*, src/filter/mod.rs,
-src/dot_product/* and src/filter/iirdes/pll, the same `pub fn` names, generic
+src/dot_product/*, src/filter/iirdes/pll and src/fft/mod.rs, the same `pub fn` names, generic
 parameters, parameter lists (names and types) and return types, the same trait
 methods and the same public structs / enums with the same variants; firdes offers a
 subset of the reference's functions with identical signatures.  The reference's

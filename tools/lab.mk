@@ -4,7 +4,6 @@
 # unchanged and adds launchers for other compile-time variants, selected by the
 # sdsp_lab_* entry points the tools/*_ab.py / *_lab.py drivers call).
 #   make -f tools/lab.mk -j8
-#   make -f tools/lab.mk archive_r03   (the frozen round-3 overlap-save lab kernels)
 HIPCC ?= /opt/rocm/bin/hipcc
 CSRC = solid_dsp_amd/csrc
 OBJ = solid_dsp_amd/_build/obj
@@ -31,14 +30,4 @@ tools/_build/lab/iir_lab.o: HIPFLAGS += -fno-slp-vectorize
 $(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_TUS)) $(PRODUCT_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@.tmp $^ && mv -f $@.tmp $@
 
-# round-3 archive: the slot / pair / trio / quad / queue kernels (sdsp_lab_set_ols_variant
-# variants >= 256 of that round)
-ARCH_OUT = tools/_build/libsdsp_lab_r03.so
-ARCH_KEEP = $(filter-out $(OBJ)/kern_fir_ols_os.o,$(wildcard $(OBJ)/*.o))
-tools/_build/lab/kern_fir_ols_os_r03.o: tools/lab/archive_r03/kern_fir_ols_os_r03.hip
-	@mkdir -p tools/_build/lab
-	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-atomic-optimizer-strategy=None -c $< -o $@
-archive_r03: tools/_build/lab/kern_fir_ols_os_r03.o
-	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $(ARCH_OUT) $< $(ARCH_KEEP)
-
-.PHONY: all archive_r03
+.PHONY: all

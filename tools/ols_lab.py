@@ -32,6 +32,7 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
     from solid_dsp_amd.filter import firdes
     L = sd.lib()
     L.sdsp_lab_set_ols_variant.argtypes = [C.c_int, C.c_int, C.c_int]
+    L.sdsp_lab_ols_stamps.argtypes = [C.c_void_p]
     if os.environ.get("OLS_HWID"):  # which CU slots the lab tickets use: distinct (XCC_ID, HW_ID[15:8])
         nb = 4096
         hb = torch.zeros(2 * nb, dtype=torch.int32, device="cuda")
@@ -94,6 +95,27 @@ def main(rounds=int(os.environ.get("OLS_ROUNDS", "15")), log2n=30):
             e1.record(s)
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / burst)
+    clocks = {}
+    for v in variants:  # in-kernel clock of the stamped variant, after a sustained burst
+        if v[0] < 0 or not (v[0] & 262144):
+            continue
+        L.sdsp_lab_set_ols_variant(*v)
+        L.sdsp_lab_ols_stamps_clear()
+        for _ in range(max(burst, 20)):
+            f.execute_block_device(d_in, n, d_out, s)
+        torch.cuda.synchronize()
+        st = np.zeros(4 * 8192, dtype=np.uint64)
+        assert L.sdsp_lab_ols_stamps(C.c_void_p(st.ctypes.data)) == 0
+        st = st.reshape(-1, 4).astype(np.float64)
+        ok = st[:, 3] > st[:, 1]
+        ghz = (st[ok, 2] - st[ok, 0]) / (st[ok, 3] - st[ok, 1]) * 0.1
+        dur_us = (st[ok, 3] - st[ok, 1]) * 0.01
+        clocks["var%d:%d:%d" % v] = {"workgroups": int(ok.sum()), "clock_GHz_median": float(np.median(ghz)),
+                                     "clock_GHz_p10": float(np.percentile(ghz, 10)),
+                                     "clock_GHz_p90": float(np.percentile(ghz, 90)),
+                                     "workgroup_us_median": float(np.median(dur_us))}
+    if clocks:
+        print("in-kernel clock (s_memtime / s_memrealtime x 100 MHz):", json.dumps(clocks, indent=1), flush=True)
     res = {("nco" if v[0] < 0 else "var%d:%d:%d" % v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                        "frac_of_8TBps": 16.0 * n / (np.median(t) * 1e-3) / 8e12,
                        "rel_diff_vs_var0": diff.get(v)} for v, t in times.items()}

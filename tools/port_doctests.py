@@ -196,6 +196,19 @@ def _round(v):  # f64::round: half away from zero
 '''
 
 
+_CTOR = re.compile(r"\b(FIRFilter|DecimatingFIRFilter)\.new\(")
+
+
+def _with_host_step(line):
+    """add host_step=host_step to every FIRFilter / DecimatingFIRFilter constructor call"""
+    out, i = "", 0
+    for m in _CTOR.finditer(line):
+        j = _close_paren(line, m.end() - 1)
+        out += line[i:j] + ", host_step=host_step)"
+        i = j + 1
+    return out + line[i:]
+
+
 def main():
     parts = ["// Generated by tools/port_doctests.py from the reference's doc comments (juliantos/solid-dsp",
              "// src/filter/{fir,iir}/*.rs, src/dot_product/*.rs): each doctest, body unchanged, as an",
@@ -221,10 +234,20 @@ def main():
     for f in FILES:
         tag = f.replace("/", "_").replace(".rs", "")
         for start, body in doctests(os.path.join(REF, f)):
+            lines = to_python(body)
+            # FIR / decimator doctests also run with host_step=False, so the
+            # reference's literals reach the HIP kernels (fir_step_kernel, the block kernels),
+            # not only the host step that short blocks and per-sample calls default to
+            dev = [_with_host_step(ln) for ln in lines]
             py.append("")
-            py.append("def test_%s_l%d():" % (tag, start))
+            if dev != lines:
+                py.append('@pytest.mark.parametrize("host_step", [None, False])')
+                py.append("def test_%s_l%d(host_step):" % (tag, start))
+                lines = dev
+            else:
+                py.append("def test_%s_l%d():" % (tag, start))
             py.append('    """src/%s:%d"""' % (f, start))
-            py += ["    " + ln for ln in to_python(body)] or ["    pass"]
+            py += ["    " + ln for ln in lines] or ["    pass"]
             py.append("")
     with open(OUT_PY, "w") as fh:
         fh.write("\n".join(py))

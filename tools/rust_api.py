@@ -27,6 +27,7 @@ FILES = {
     "dot_product/execute.rs": ("dot_product/execute.rs", "eq"),
     "filter/iirdes/pll/mod.rs": ("filter/iirdes/pll/mod.rs", "eq"),
     "filter/firdes/mod.rs": ("filter/firdes/mod.rs", "sub"),
+    "fft/mod.rs": ("fft.rs", "eq"),
 }
 
 
