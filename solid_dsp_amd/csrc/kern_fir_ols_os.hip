@@ -110,7 +110,10 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // (ablation: no transform); 128 plain (not nontemporal) stores; 256 input rows
 // loaded last to first; 512 output rows stored last to first; 1024 each XCD walks the
 // even segments of its eighth, then the odd ones (a segment's halo row is then read
-// long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss);
+// long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss); 2097152 rows
+// loaded in row order (the product loads them in the first radix-4 stage's order); 4194304 the
+// twiddle-base tables requested after the rows; 8388608 no boundary / history code (timing only:
+// the first segment reads zeros before the stream and the history is not written);
 // ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
 // twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores; 16384
 // plain (not nontemporal) input loads; 32768 all six twiddle bases loaded (the round-3 form;
@@ -145,16 +148,47 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         }
     };
     float4 tq[6];  // the raw table loads (products formed once the rows are requested)
-    if constexpr ((ABL & (32768 | 4096)) == 0) {
-        tq[0] = tab(t, 16 * kOlsOsTabCD), tq[1] = tab(lo4, 16 * kOlsOsTabEF);
-    } else {
-        tq[0] = tab(t, 0), tq[1] = tab(t, 4096), tq[2] = tab(t, 8192);
-        tq[3] = tab(lo4, 12288), tq[4] = tab(lo4, 12544), tq[5] = tab(lo4, 12800);
-    }
+    auto load_tables = [&] {
+        if constexpr ((ABL & (32768 | 4096)) == 0) {
+            tq[0] = tab(t, 16 * kOlsOsTabCD), tq[1] = tab(lo4, 16 * kOlsOsTabEF);
+        } else {
+            tq[0] = tab(t, 0), tq[1] = tab(t, 4096), tq[2] = tab(t, 8192);
+            tq[3] = tab(lo4, 12288), tq[4] = tab(lo4, 12544), tq[5] = tab(lo4, 12800);
+        }
+    };
+    if constexpr ((ABL & 4194304) == 0) load_tables();
     f2 v[16];
-    if (base < 0) {
-        // rows before the stream come from the handle's history (the last Lm1 inputs, oldest
-        // first); positions before the history read as 0 (an out-of-range offset)
+    // The segment's rows, for every segment through the same loads (a window that starts before
+    // the stream reads zeros here, through an empty descriptor, and is completed below), in the
+    // order the first radix-4 stage consumes them (rows nb, 4 + nb, 8 + nb, 12 + nb for nb = 0..3:
+    // its first butterflies start after four rows have landed).  A branch around these loads
+    // would join with the boundary path before P1 and make the compiler wait for every row there.
+    const auto rxl = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, base < 0 ? 0 : nrec, kBufWord3);
+    if constexpr ((ABL & 524288) != 0) {
+        // 16-byte lanes: lane t = 2c + h loads columns (2c, 2c + 1) of rows k + 8h, then one DPP
+        // exchange per dword with its partner lane t ^ 1 gives it column t over the 16 rows
+        f4v q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            q[k] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rxl, 16 * (t >> 1) + 16384 * (t & 1),
+                                                                                2048 * k, kLdAux));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pair_exchange(f2{q[k].x, q[k].y}, f2{q[k].z, q[k].w}, v[k], v[8 + k]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int r = (ABL & 256) ? 15 - i : (ABL & 2097152) ? i : 4 * (i & 3) + (i >> 2);
+            if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
+            else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
+            else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rxl, 8 * t, 2048 * r, kLdAux));
+        }
+    }
+    if constexpr ((ABL & 4194304) != 0) load_tables();  // lab: the tables after the rows
+    if ((ABL & 8388608) == 0 && base < 0) {
+        // the first segments: rows inside the stream again through rx, rows before it from the
+        // handle's history (the last Lm1 inputs, oldest first; positions before the history read
+        // as 0 through an out-of-range offset).  Waits for its loads before the join, so the
+        // interior path keeps its partial waits.
         const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)hist, (short)0, 8 * Lm1, kBufWord3);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -166,24 +200,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
                 v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rp, e >= 0 ? (int)(8 * e) : 0x7ffffff0, 0, 0));
             }
         }
-    } else if constexpr ((ABL & 524288) != 0) {
-        // 16-byte lanes: lane t = 2c + h loads columns (2c, 2c + 1) of rows k + 8h, then one DPP
-        // exchange per dword with its partner lane t ^ 1 gives it column t over the 16 rows
-        f4v q[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            q[k] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, 16 * (t >> 1) + 16384 * (t & 1),
-                                                                                2048 * k, kLdAux));
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pair_exchange(f2{q[k].x, q[k].y}, f2{q[k].z, q[k].w}, v[k], v[8 + k]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int r = (ABL & 256) ? 15 - i : i;
-            if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
-            else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
-            else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, kLdAux));
-        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     }
     if constexpr ((ABL & 4) && (ABL & 131072)) {
         // HBM-only with the NCO kernel's lane shape: the segment as eight 4 KB rows of 16-byte
@@ -231,7 +248,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         Eb[0] = f2{e0.x, e0.y}, Eb[1] = f2{e0.z, e0.w}, Eb[2] = f2{e1.x, e1.y};
         Fa[0] = f2{e1.z, e1.w}, Fa[1] = f2{e2.x, e2.y}, Fa[2] = f2{e2.z, e2.w};
     }
-    if (new_hist != nullptr) {
+    if ((ABL & 8388608) == 0 && new_hist != nullptr) {
         // the call's last segment: its window holds the last Lm1 inputs (halo >= Lm1), which
         // become the history of the next call (ping-pong buffer: never the one read above)
         const long long h0 = n - Lm1;

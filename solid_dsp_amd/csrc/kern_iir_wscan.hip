@@ -81,6 +81,15 @@ __device__ __forceinline__ I sos_step_f(const C* __restrict__ c, I v, I (&w1)[S]
     return v;
 }
 
+// the state scales of an SOS group's wave-scan coefficient set (see sys_step): state d of the
+// kernel = the reference's state d * wscan_inv(d); the reference's = the kernel's * wscan_scale(d)
+template <int S, typename C> __device__ __forceinline__ C wscan_scale(const C* __restrict__ c, int d) {
+    return c[5 * S + d];
+}
+template <int S, typename C> __device__ __forceinline__ C wscan_inv(const C* __restrict__ c, int d) {
+    return c[5 * S + 2 * S + d];
+}
+
 // y = P x for a lower block-triangular P (2x2 blocks), wave-uniform
 template <int D, typename C, typename I>
 __device__ __forceinline__ void matvec_lt(const C* __restrict__ P, const I (&x)[D], I (&y)[D]) {
@@ -110,13 +119,23 @@ __device__ __forceinline__ void matvec_full(const C* __restrict__ P, const I (&x
 // (src/filter/iir/mod.rs:272-279) with ND states hh[i] = v[n-1-i]; coefficients
 // num[0..ND] then den[0..ND) (a[1..] / a0), zero padded to those lengths:
 //   v = x - den . hh,   y = num[0] v + num[1..] . hh,   hh <- (v, hh[0..ND-2])
+//
+// SOS cascades run in b0-factored coordinates (runtime_iir.cpp wscan_coefs): the
+// wave-scan coefficient set of a group holds, for every section but the last, (1, b1/b0, b2/b0,
+// a1, a2), so the section's output is w + b1' w1 + b2' w2 (two fused multiply-adds instead of a
+// multiply and two), and the last section carries the product G of the b0 before it: (G b0, G b1,
+// G b2, a1, a2).  Section q's state is then the reference's divided by G_q = prod_{j<q} b0_j:
+// the D scales G_q and their inverses follow the 5 S coefficients (wscan_scale / _inv), applied
+// where a call's state enters (st_in) and leaves (st_out), so the handle's state buffer stays in
+// the reference's units.
 template <int S, int ND, typename C, typename I>
 __device__ __forceinline__ I sys_step(const C* __restrict__ c, I v, I (&st)[ND ? ND : 2 * S]) {
     if constexpr (ND == 0) {
 #pragma unroll
         for (int q = 0; q < S; ++q) {
             const I w = fmac_(fmac_(v, -c[5 * q + 4], st[2 * q + 1]), -c[5 * q + 3], st[2 * q]);
-            v = fmac_(fmac_(mul_(c[5 * q + 2], st[2 * q + 1]), c[5 * q + 1], st[2 * q]), c[5 * q + 0], w);
+            if (q + 1 < S) v = fmac_(fmac_(w, c[5 * q + 1], st[2 * q]), c[5 * q + 2], st[2 * q + 1]);
+            else v = fmac_(fmac_(mul_(c[5 * q + 2], st[2 * q + 1]), c[5 * q + 1], st[2 * q]), c[5 * q + 0], w);
             st[2 * q + 1] = st[2 * q];
             st[2 * q] = w;
         }
@@ -173,7 +192,7 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // kernels are LAB = 0): ablations 1 no zero-state run, 2 no scan, 4 no correction, 8 no HBM
 // loads, 16 no HBM stores; variants 32 plain (not nontemporal) loads, 64 plain stores, 128
 // nontemporal stores (the round-3 product; the product's interior stores are write-through), 256
-// the scalar correction (the round-3 arithmetic; real f32)
+// the scalar correction (the round-3 arithmetic; real f32), 512 every scan level (the round-4 scan)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -229,6 +248,12 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 #pragma unroll
     for (int d = 0; d < D; ++d) carry[d] = cin ? cin[((long long)ch * nwaves + gw) * D + d] : zero_v<I>();
     const bool agg = gagg != nullptr;  // aggregate pass: the wave's zero-carry end state only
+    // scan levels: with warm-up (wc > 0) the state response has decayed below the warm-up
+    // tolerance after wc chunks (||A^(wc B)|| < 1e-9 f32 / 1e-17 f64, the criterion that admits the
+    // scan), so a lane needs the states of the 2^nlev - 1 >= wc - 1 lanes before it only: the
+    // levels with offsets >= wc add terms below that tolerance and are skipped (cfg3: wc = 6, 3
+    // levels of 6).  The exact-carry form (wc = 0) keeps every level.
+    const int nlev = (wc > 0 && !(LAB & 512)) ? (wc > 1 ? 32 - __builtin_clz((unsigned)(wc - 1)) : 0) : 6;
 
     // interior tiles are read with straight-line 16-byte loads, one tile ahead of
     // the compute (a per-vector branch would serialise the HBM round trips)
@@ -303,7 +328,10 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         }
         if (!cin && !agg && gw == 0 && t == 0 && lane == wc - 1) {  // the call's exact carried state enters here
 #pragma unroll
-            for (int d = 0; d < D; ++d) s[d] = st_in[d];
+            for (int d = 0; d < D; ++d) {
+                if constexpr (ND == 0) s[d] = mul_(wscan_inv<S>(coefs, d), st_in[d]);
+                else s[d] = st_in[d];
+            }
         }
         // 3. fold the carry into lane 0, then the inclusive scan over lanes
         if (!(lab & 2)) {
@@ -316,6 +344,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
         }
 #pragma unroll
         for (int k = 0; k < 6 && !(lab & 2); ++k) {
+            if (k >= nlev) break;  // the terms of lanes >= 2^nlev back have decayed (see nlev)
             const int off = 1 << k;
             I prev[D], a[D];
 #pragma unroll
@@ -406,7 +435,10 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             for (int d = 0; d < D; ++d) st[d] = init[d];
             for (long long k = kc; k < nd; ++k) (void)sys_step<S, ND>(coefs, dom(k), st);
 #pragma unroll
-            for (int d = 0; d < D; ++d) st_out[d] = st[d];
+            for (int d = 0; d < D; ++d) {
+                if constexpr (ND == 0) st_out[d] = mul_(wscan_scale<S>(coefs, d), st[d]);
+                else st_out[d] = st[d];
+            }
         }
         wave_sync();
 
@@ -462,10 +494,10 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 // contiguous run of R waves (Horner with Phi), lane 0 chains the 256 run
 // aggregates with Phi^R, then every lane replays its run from its exact prefix.
 
-template <int D, typename C, typename I>
+template <int D, int S, typename C, typename I>
 __global__ void __launch_bounds__(256)
 wscan_carry_kernel(const I* __restrict__ G, I* __restrict__ cin, const C* __restrict__ Phi, const I* __restrict__ st_in,
-                   long long W) {
+                   long long W, const C* __restrict__ coefs) {
     __shared__ C sPhi[D * D], sPhiR[D * D];
     __shared__ I agg[256][D];
     const int t = threadIdx.x, ch = blockIdx.x;
@@ -517,7 +549,10 @@ wscan_carry_kernel(const I* __restrict__ G, I* __restrict__ cin, const C* __rest
     if (t == 0) {  // exclusive prefixes over runs: p_{j+1} = Phi^R p_j + agg_j
         I p[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) p[d] = st_in[d];
+        for (int d = 0; d < D; ++d) {  // S > 0: an SOS group in b0-factored coordinates (sys_step)
+            if constexpr (S > 0) p[d] = mul_(wscan_inv<S>(coefs, d), st_in[d]);
+            else p[d] = st_in[d];
+        }
         for (int j = 0; j < 256; ++j) {
             I q[D];
 #pragma unroll
@@ -684,10 +719,10 @@ sos_wscan2_kernel(const float* __restrict__ x, float* __restrict__ y, const floa
             const int vl = wc - 1;
             if (vl < 64 && lane == vl) {
 #pragma unroll
-                for (int d = 0; d < D; ++d) s[d].x = st_in[d];
+                for (int d = 0; d < D; ++d) s[d].x = wscan_inv<S>(coefs, d) * st_in[d];
             } else if (vl >= 64 && lane == vl - 64) {
 #pragma unroll
-                for (int d = 0; d < D; ++d) s[d].y = st_in[d];
+                for (int d = 0; d < D; ++d) s[d].y = wscan_inv<S>(coefs, d) * st_in[d];
             }
         }
         // carry into virtual lane 0
@@ -776,7 +811,10 @@ sos_wscan2_kernel(const float* __restrict__ x, float* __restrict__ y, const floa
                 }
                 for (long long k = kc; k < nd; ++k) (void)sos_step_f<S>(coefs, x[k], w1, w2);
 #pragma unroll
-                for (int q = 0; q < S; ++q) { st_out[2 * q] = w1[q]; st_out[2 * q + 1] = w2[q]; }
+                for (int q = 0; q < S; ++q) {
+                    st_out[2 * q] = wscan_scale<S>(coefs, 2 * q) * w1[q];
+                    st_out[2 * q + 1] = wscan_scale<S>(coefs, 2 * q + 1) * w2[q];
+                }
             }
         }
         wave_sync();
@@ -871,9 +909,9 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st, int tpw_force = 0) {
         hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
                            (I*)a.y, (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out,
                            nd, 0, tpw, vec_ok, a.Mi, a.Md, j0, ny, (const I*)nullptr, (I*)a.G, waves);
-        hipLaunchKernelGGL((wscan_carry_kernel<D, C, I>), dim3((unsigned)a.channels), dim3(256), 0, st,
+        hipLaunchKernelGGL((wscan_carry_kernel<D, ND ? 0 : S, C, I>), dim3((unsigned)a.channels), dim3(256), 0, st,
                            (const I*)a.G, (I*)a.Cin, (const C*)a.Phi + (size_t)(tpw - 1) * D * D, (const I*)a.st_in,
-                           waves);
+                           waves, (const C*)a.coefs);
     }
     hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,

@@ -41,6 +41,12 @@ struct Group {
         DevBuf d_Phi;          // exact carries: [8][2c][2c] A^(64 B t), t = 1..8
         long long phi_wmax[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // per tpw: waves the carry chain admits
     } ws[6];
+    // SOS wave scan in b0-factored coordinates (kern_iir_wscan.hip sys_step): the group's
+    // coefficients (1, b1/b0, b2/b0, a1, a2) per section, (G b0, G b1, G b2, a1, a2) for the last
+    // (G = prod of the b0 before it), and on the device the state scales G_q and their inverses
+    std::vector<double> wc64;
+    std::vector<double> wscale;  // [2 count]: reference state = kernel state * wscale
+    DevBuf d_wcoefs;
 };
 
 struct DeviceGuardI {
@@ -152,8 +158,10 @@ int group_dim(const sdsp_iir* h, const Group& g) { return h->type == 1 ? 2 * g.c
 // [first, first+count) of the SOS cascade (sos.rs:92-114), or the Normal DF-II
 // recurrence (mod.rs:272-279).  The coefficients are the handle's (already rounded
 // to the Coef type), so T = float reproduces an f32 handle's arithmetic.
+// cf: the group's SOS coefficients, 5 per section (the handle's normalised ones, or the wave
+// scan's b0-factored set, group_coefs)
 template <typename T>
-void sys_run(const sdsp_iir* h, const Group& g, const T* x, T* y, size_t n, std::vector<T>& s) {
+void sys_run(const sdsp_iir* h, const Group& g, const double* cf, const T* x, T* y, size_t n, std::vector<T>& s) {
     if (h->type == 0) {
         const int D = h->cap - 1, nb = h->nb, na1 = h->na - 1;
         const double* num = h->c64.data();
@@ -173,7 +181,7 @@ void sys_run(const sdsp_iir* h, const Group& g, const T* x, T* y, size_t n, std:
     for (size_t i = 0; i < n; ++i) {
         T v = x[i];
         for (int q = 0; q < g.count; ++q) {
-            const double* c = &h->c64[5 * (g.first + q)];
+            const double* c = cf + 5 * q;
             const T w = v - ((T)c[3] * s[2 * q] + (T)c[4] * s[2 * q + 1]);
             v = (T)c[0] * w + (T)c[1] * s[2 * q] + (T)c[2] * s[2 * q + 1];
             s[2 * q + 1] = s[2 * q];
@@ -183,15 +191,22 @@ void sys_run(const sdsp_iir* h, const Group& g, const T* x, T* y, size_t n, std:
     }
 }
 
+// the coefficients a group's system runs on: the wave scan's b0-factored set (scaled, SOS only)
+// or the handle's normalised coefficients
+const double* group_coefs(const sdsp_iir* h, const Group& g, bool scaled) {
+    if (h->type != 1) return nullptr;
+    return scaled ? g.wc64.data() : &h->c64[5 * (size_t)g.first];
+}
+
 // state-transition matrix of the group's system (zero input), row-major
-Mat sys_A(const sdsp_iir* h, const Group& g) {
+Mat sys_A(const sdsp_iir* h, const Group& g, const double* cf) {
     const int D = group_dim(h, g);
     Mat A(D * D, 0.0);
     const double zero = 0.0;
     for (int j = 0; j < D; ++j) {
         std::vector<double> s(D, 0.0);
         s[j] = 1.0;
-        sys_run<double>(h, g, &zero, nullptr, 1, s);
+        sys_run<double>(h, g, cf, &zero, nullptr, 1, s);
         for (int i = 0; i < D; ++i) A[i * D + j] = s[i];
     }
     return A;
@@ -218,7 +233,7 @@ double probe_rel(const std::vector<T>& a, const std::vector<double>& ref) {
 }
 
 template <typename T>
-bool carry_well_conditioned_t(const sdsp_iir* h, const Group& g, int B, const Mat& AB) {
+bool carry_well_conditioned_t(const sdsp_iir* h, const Group& g, const double* cf, int B, const Mat& AB) {
     const int D = group_dim(h, g);
     const size_t n = 1 << 14;
     std::vector<double> x64(n), ref(n);
@@ -228,21 +243,21 @@ bool carry_well_conditioned_t(const sdsp_iir* h, const Group& g, int B, const Ma
         v = (double)(float)((double)(r >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0);
     }
     std::vector<double> s64(D, 0.0);
-    sys_run<double>(h, g, x64.data(), ref.data(), n, s64);
+    sys_run<double>(h, g, cf, x64.data(), ref.data(), n, s64);
     std::vector<T> x(x64.begin(), x64.end()), ys(n), yc(n);
     std::vector<T> st(D, 0);
-    sys_run<T>(h, g, x.data(), ys.data(), n, st);
+    sys_run<T>(h, g, cf, x.data(), ys.data(), n, st);
     std::vector<T> cr(D * (size_t)B), ABt(AB.begin(), AB.end());
     for (int d = 0; d < D; ++d) {  // Cr[i][d]: output response to basis state e_d
         std::vector<T> zs(D, 0), zero(B, 0), out(B);
         zs[d] = 1;
-        sys_run<T>(h, g, zero.data(), out.data(), B, zs);
+        sys_run<T>(h, g, cf, zero.data(), out.data(), B, zs);
         for (int i = 0; i < B; ++i) cr[(size_t)i * D + d] = out[i];
     }
     std::vector<T> I(D, 0), e(D), nI(D);
     for (size_t k = 0; k < n; k += B) {
         std::fill(e.begin(), e.end(), T(0));
-        sys_run<T>(h, g, &x[k], &yc[k], B, e);
+        sys_run<T>(h, g, cf, &x[k], &yc[k], B, e);
         for (int i = 0; i < B; ++i)
             for (int d = 0; d < D; ++d) yc[k + i] += cr[(size_t)i * D + d] * I[d];
         for (int a = 0; a < D; ++a) {
@@ -256,20 +271,21 @@ bool carry_well_conditioned_t(const sdsp_iir* h, const Group& g, int B, const Ma
     return e_car <= 10.0 * e_ser + (sizeof(T) == 8 ? 1e-13 : 1e-7);
 }
 
-bool carry_well_conditioned(const sdsp_iir* h, const Group& g, int B, const Mat& AB) {
-    return is_f32(h->dtype) ? carry_well_conditioned_t<float>(h, g, B, AB)
-                            : carry_well_conditioned_t<double>(h, g, B, AB);
+bool carry_well_conditioned(const sdsp_iir* h, const Group& g, const double* cf, int B, const Mat& AB) {
+    return is_f32(h->dtype) ? carry_well_conditioned_t<float>(h, g, cf, B, AB)
+                            : carry_well_conditioned_t<double>(h, g, cf, B, AB);
 }
 
 // Scan tables for chunks of B samples: warm-up chunks wc (smallest m with
 // ||A^(mB)||_inf < tol, m <= max_wc; 0 = the scan is not admissible), P_k =
 // A^(B 2^k) for k < nP, and optionally Cr[i][d] (i < B): the cascade output i
 // steps after starting from basis state e_d with zero input.
-int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, int* wc, DevBuf* dP, DevBuf* dCr,
-                DevBuf* dPhi = nullptr, bool* exact = nullptr) {
+int scan_tables(const sdsp_iir* h, const Group& g, bool scaled, int B, int max_wc, int nP, int* wc, DevBuf* dP,
+                DevBuf* dCr, DevBuf* dPhi = nullptr, bool* exact = nullptr) {
     const double tol = is_f32(h->dtype) ? 1e-9 : 1e-17;
     const int D = group_dim(h, g);
-    const Mat A = sys_A(h, g);
+    const double* cf = group_coefs(h, g, scaled);
+    const Mat A = sys_A(h, g, cf);
     const Mat AB = matpow(A, B, D);
     Mat Am = AB;
     *wc = 0;
@@ -280,7 +296,7 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
         Am = matmul(Am, AB, D);
     }
     if (exact) *exact = false;
-    if (*wc > 0 && h->type == 0 && !carry_well_conditioned(h, g, B, AB)) {
+    if (*wc > 0 && h->type == 0 && !carry_well_conditioned(h, g, cf, B, AB)) {
         *wc = 0;  // a direct-form polynomial whose companion powers lose digits: serial only
         return SDSP_OK;
     }
@@ -298,7 +314,7 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
             for (double v : At) push_coef(Phi, v, h->dtype);
             At = matmul(At, A64, D);
         }
-        if (!carry_well_conditioned(h, g, B, AB)) return SDSP_OK;
+        if (!carry_well_conditioned(h, g, cf, B, AB)) return SDSP_OK;
         IIR_TRY(dPhi->ensure(Phi.size()), "alloc Phi");
         IIR_TRY(hipMemcpy(dPhi->p, Phi.data(), Phi.size(), hipMemcpyHostToDevice), "copy Phi");
         *exact = true;
@@ -316,7 +332,7 @@ int scan_tables(const sdsp_iir* h, const Group& g, int B, int max_wc, int nP, in
     for (int d = 0; d < D; ++d) {  // output response to basis state e_d, zero input
         std::vector<double> st(D, 0.0), zero(B, 0.0), out(B);
         st[d] = 1.0;
-        sys_run<double>(h, g, zero.data(), out.data(), B, st);
+        sys_run<double>(h, g, cf, zero.data(), out.data(), B, st);
         for (int i = 0; i < B; ++i) resp[(size_t)i * D + d] = out[i];
     }
     std::vector<unsigned char> Cr;
@@ -350,7 +366,7 @@ bool exact_carry_bounded(const sdsp_iir* h, Group& g, int wv, size_t waves, int 
     long long& wmax = g.ws[wv].phi_wmax[tpw];
     if (wmax < 0) {
         const int D = group_dim(h, g), B = iir_wscan_chunk(h->dtype, wv);
-        Mat P = matpow(matpow(sys_A(h, g), B, D), 64LL * tpw, D);
+        Mat P = matpow(matpow(sys_A(h, g, group_coefs(h, g, true)), B, D), 64LL * tpw, D);
         wmax = 0;
         double bound = 1.0;  // >= ||Phi^m||_inf for every m < 2^(j+1)
         for (int j = 0; j < 48; ++j) {
@@ -365,6 +381,41 @@ bool exact_carry_bounded(const sdsp_iir* h, Group& g, int wv, size_t waves, int 
     return (long long)waves <= wmax;
 }
 
+// The wave scan's b0-factored coefficient set of an SOS group (kern_iir_wscan.hip sys_step):
+// section q < count - 1 runs w = v - a1 w1 - a2 w2, out = w + (b1/b0) w1 + (b2/b0) w2 on states
+// divided by G_q = prod_{j<q} b0_j, and the last section (G b0, G b1, G b2) gives the reference's
+// output.  Saves one multiply per section but the last per sample (cfg3: 20 -> 17 operations in
+// the zero-state run).  The values are formed in f64 from the handle's normalised coefficients and
+// rounded to the Coef type once.  False when a section but the last has b0 = 0 or a scale leaves
+// [1e-30, 1e30].
+bool wscan_coefs(const sdsp_iir* h, Group& g) {
+    g.wc64.assign(5 * (size_t)g.count, 0.0);
+    g.wscale.assign(2 * (size_t)g.count, 1.0);
+    double G = 1.0;
+    for (int q = 0; q < g.count; ++q) {
+        const double* c = &h->c64[5 * (size_t)(g.first + q)];
+        double* o = &g.wc64[5 * (size_t)q];
+        g.wscale[2 * q] = g.wscale[2 * q + 1] = G;
+        if (!(std::fabs(G) >= 1e-30 && std::fabs(G) <= 1e30)) return false;
+        o[3] = c[3];
+        o[4] = c[4];
+        if (q + 1 < g.count) {
+            if (c[0] == 0.0 || !std::isfinite(c[1] / c[0]) || !std::isfinite(c[2] / c[0])) return false;
+            o[0] = 1.0;
+            o[1] = c[1] / c[0];
+            o[2] = c[2] / c[0];
+            G *= c[0];
+        } else {
+            o[0] = G * c[0];
+            o[1] = G * c[1];
+            o[2] = G * c[2];
+        }
+    }
+    if (!is_f32(h->dtype)) return true;
+    for (double& v : g.wc64) v = (double)(float)v;  // the values the f32 kernel multiplies by
+    return true;
+}
+
 int plan_groups(sdsp_iir* h) {
     h->groups.clear();
     if (h->type == 0) {  // Normal DF-II: one dense system of cap - 1 states on the wave scan (D <= 8)
@@ -373,7 +424,7 @@ int plan_groups(sdsp_iir* h) {
         h->groups.emplace_back();
         Group& g = h->groups.back();
         const int Bw = iir_wscan_chunk(h->dtype, 0);
-        int st = scan_tables(h, g, Bw, 32, 7, &g.ws[0].wc, &g.ws[0].d_P, &g.ws[0].d_Cr, &g.ws[0].d_Phi,
+        int st = scan_tables(h, g, false, Bw, 32, 7, &g.ws[0].wc, &g.ws[0].d_P, &g.ws[0].d_Cr, &g.ws[0].d_Phi,
                              &g.ws[0].exact);
         if (st) return st;
         // the kernel's coefficient layout: num[0..D] then den[0..D), zero padded
@@ -391,18 +442,27 @@ int plan_groups(sdsp_iir* h) {
         g.first = f;
         g.count = std::min(kMaxGroupSections, h->S - f);
         // block scan (kern_iir.hip): 8 powers, warm-up up to half the block's lanes
-        int st = scan_tables(h, g, iir_scan_chunk(h->dtype), kScanLanes / 2, 8, &g.wc, &g.d_P, nullptr);
+        int st = scan_tables(h, g, false, iir_scan_chunk(h->dtype), kScanLanes / 2, 8, &g.wc, &g.d_P, nullptr);
         if (st) return st;
-        // wave scan (kern_iir_wscan.hip), one table set per chunk size: 6 powers, warm-up <= 32
-        // chunks; without a decaying state response the single-chunk variants carry exactly
+        // wave scan (kern_iir_wscan.hip) in b0-factored coordinates; a section other than the last
+        // with b0 = 0 (or scales out of range) has no such form: its group stays off the wave scan
+        if (!wscan_coefs(h, g)) continue;
+        // one table set per chunk size: 6 powers, warm-up <= 32 chunks; without a decaying state
+        // response the single-chunk variants carry exactly
         for (int v = 0; v < 6; ++v) {
             const int Bw = iir_wscan_chunk(h->dtype, v);
             if (Bw == 0) continue;
             if (g.wc == 0 && v != 0 && v != 1) continue;
-            st = scan_tables(h, g, Bw, 32, 7, &g.ws[v].wc, &g.ws[v].d_P, &g.ws[v].d_Cr, &g.ws[v].d_Phi,
+            st = scan_tables(h, g, true, Bw, 32, 7, &g.ws[v].wc, &g.ws[v].d_P, &g.ws[v].d_Cr, &g.ws[v].d_Phi,
                              &g.ws[v].exact);
             if (st) return st;
         }
+        std::vector<unsigned char> c;  // device layout: 5 count coefficients, count * 2 scales, inverses
+        for (double v : g.wc64) push_coef(c, v, h->dtype);
+        for (double v : g.wscale) push_coef(c, v, h->dtype);
+        for (double v : g.wscale) push_coef(c, 1.0 / v, h->dtype);
+        IIR_TRY(g.d_wcoefs.ensure(c.size()), "alloc wave-scan coefs");
+        IIR_TRY(hipMemcpy(g.d_wcoefs.p, c.data(), c.size(), hipMemcpyHostToDevice), "copy wave-scan coefs");
     }
     return SDSP_OK;
 }
@@ -567,6 +627,7 @@ void sdsp_iir_destroy(sdsp_iir* h) {
         for (int i = 0; i < 2; ++i) { h->d_state[i].release(); h->d_tmp[i].release(); h->d_carry[i].release(); }
         for (auto& g : h->groups) {
             g.d_P.release();
+            g.d_wcoefs.release();
             for (auto& w : g.ws) { w.d_P.release(); w.d_Cr.release(); w.d_Phi.release(); }
         }
         h->stage_in.release();
@@ -723,6 +784,7 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
                 wave_scan = exact_carry_bounded(h, gr, wv, W, tpw);
             }
             if (wave_scan) {
+                a.coefs = gr.d_wcoefs.p;  // the b0-factored set (sys_step)
                 a.P = gr.ws[wv].d_P.p;
                 a.Cr = gr.ws[wv].d_Cr.p;
                 a.wc = gr.ws[wv].wc;

@@ -136,13 +136,18 @@ struct StreamFence {
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
     }
+    // A marker on the legacy default stream is recorded through its null handle: an event
+    // recorded on the special handle hipStreamLegacy makes every later hipStreamWaitEvent on
+    // it crash inside the runtime (SIGSEGV, any waiting stream), while one recorded on the null
+    // stream is waited for normally (tools/fence_probe.hip, profiles/r05/fence_probe.log: the
+    // round-4 AutoCorrelator crash, a block on torch's default stream followed by get_energy)
     hipError_t record(hipStream_t s) {
         const int nxt = (cur + 1) % kRing;
         if (!ev[nxt]) {
             hipError_t e = hipEventCreateWithFlags(&ev[nxt], hipEventDisableTiming);
             if (e != hipSuccess) return e;
         }
-        hipError_t e = hipEventRecord(ev[nxt], s);
+        hipError_t e = hipEventRecord(ev[nxt], legacy(s) ? nullptr : s);
         if (e != hipSuccess) return e;
         cur = nxt;
         pending = true;
@@ -150,13 +155,11 @@ struct StreamFence {
         return hipSuccess;
     }
     // order work about to be queued on `s` after the pending marker (nothing to do on the
-    // marker's own stream: stream order).  A marker on, or a wait from, the legacy null
-    // stream is waited for on the host instead: a device-side wait across it crashed the
-    // host side of the runtime in a round-4 GPU run (AutoCorrelator block on the legacy
-    // stream, then get_energy on the handle's stream)
+    // marker's own stream: stream order; the null handle and hipStreamLegacy are the same
+    // stream).  Device-side waits from any stream, the legacy one included (record() keeps the
+    // marker off the hipStreamLegacy handle)
     hipError_t order_before(hipStream_t s) {
-        if (!pending || s == stream) return hipSuccess;
-        if (legacy(s) || legacy(stream)) return wait();
+        if (!pending || s == stream || (legacy(s) && legacy(stream))) return hipSuccess;
         return hipStreamWaitEvent(s, ev[cur], 0);
     }
     static bool legacy(hipStream_t s) { return s == nullptr || s == hipStreamLegacy; }

@@ -84,6 +84,10 @@ class _FirBase:
     def set_algo(self, algo: int):
         L.check(L.lib().sdsp_fir_set_algo(self._h, algo))
 
+    def set_tuning(self, key: int, value: int):
+        """kernel-variant knobs (SDSP_TUNE_*, include/sdsp.h): performance only"""
+        L.check(L.lib().sdsp_fir_set_tuning(self._h, int(key), int(value)))
+
     def set_host_step(self, on: bool, block_macs: int = None):
         """execute(sample), push and host blocks of n * len <= block_macs multiply-adds on the host
         against the handle's delay line (True, the default) or as device launches (False)."""

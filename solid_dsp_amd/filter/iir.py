@@ -81,6 +81,10 @@ class _IirBase:
     def set_algo(self, algo):
         L.check(L.lib().sdsp_iir_set_algo(self._h, algo))
 
+    def set_tuning(self, key: int, value: int):
+        """kernel-variant knobs (SDSP_TUNE_*, include/sdsp.h): performance only"""
+        L.check(L.lib().sdsp_iir_set_tuning(self._h, int(key), int(value)))
+
     def scan_info(self, group=0):
         wc, ch = C.c_int(0), C.c_int(0)
         L.check(L.lib().sdsp_iir_scan_info(self._h, group, C.byref(wc), C.byref(ch)))

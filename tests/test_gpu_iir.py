@@ -499,3 +499,63 @@ def test_default_handle_is_exact_on_large_blocks():
     f = IIRFilter(ff, fb, SO, sample_dtype=np.float32)
     o = O.iir(O.RR32, ff, fb, O.SECOND_ORDER)
     assert bits_equal(f.execute_block(x), o.execute_block(x))
+
+
+def test_iir_time_shard_exchange_on_device():
+    """bench.py --config 3 --shard time on one device.  Three segments of one
+    butter(8) stream run from zero state on device handles (f32, the wave scan); their final
+    states (get_state) joined by parallel.iir_exclusive_scan, and the zero-input response of
+    each true initial state (a second handle after set_state, over zeros) added to the first W
+    outputs, reproduce the whole stream's f64 restatement within the scan tolerance.  Also
+    pins the device state layout against parallel.sos_state_space: from a random set_state, a
+    device block's outputs and final state are c A^k s0 + zero-state response and A^n s0 + s_n."""
+    from solid_dsp_amd import parallel as P
+    ff, fb = butter()
+    ff32, fb32 = ff.astype(np.float32), fb.astype(np.float32)
+    A, b, c, d = P.sos_state_space(ff32.astype(np.float64), fb32.astype(np.float64))
+    n, R = 1 << 18, 3
+    x = O.synth(20250226, 0, 0, R * n).astype(np.float32)
+    ref = O.iir(O.RR64, ff32.astype(np.float64), fb32.astype(np.float64), O.SECOND_ORDER).execute_block(
+        x.astype(np.float64))
+    Phi = P.state_transition(A, n)
+    W = P.zero_input_length(A, c, n)
+    y0, states = [], []
+    for r in range(R):
+        f = IIRFilter(ff32, fb32, SO, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+        y0.append(f.execute_block(x[r * n:(r + 1) * n]))
+        states.append(f.get_state()[0].astype(np.float64))
+    init = P.iir_exclusive_scan(states, Phi)
+    g = IIRFilter(ff32, fb32, SO, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+    out = []
+    for r in range(R):
+        g.set_state(init[r].astype(np.float32))
+        corr = g.execute_block(np.zeros(W, np.float32))
+        y = y0[r].astype(np.float64)
+        y[:W] += corr
+        out.append(y)
+    got = np.concatenate(out)
+    assert rel_rms(got, ref) <= 1e-5, rel_rms(got, ref)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+    # the state layout: a block from a random state against the f64 state-space model
+    rng = np.random.default_rng(3)
+    s0 = rng.standard_normal(A.shape[0]).astype(np.float32)
+    m = 1 << 16
+    xs = x[:m]
+    h = IIRFilter(ff32, fb32, SO, sample_dtype=np.float32, algo=sd.ALGO_FMA)
+    h.set_state(s0)
+    ys = h.execute_block(xs)
+    s_end = h.get_state()[0].astype(np.float64)
+    zs = O.iir(O.RR64, ff32.astype(np.float64), fb32.astype(np.float64), O.SECOND_ORDER)
+    yz = zs.execute_block(xs.astype(np.float64))
+    resp = np.empty(m)
+    st = s0.astype(np.float64)
+    for k in range(m):  # c A^k s0
+        resp[k] = c @ st
+        st = A @ st
+    yref = yz + resp
+    assert rel_rms(ys, yref) <= 1e-5, rel_rms(ys, yref)
+    s_zero = np.zeros(A.shape[0])
+    for k in range(m):
+        s_zero = A @ s_zero + b * float(xs[k])
+    s_ref = st + s_zero
+    assert np.linalg.norm(s_end - s_ref) <= 1e-5 * max(np.linalg.norm(s_ref), 1.0)

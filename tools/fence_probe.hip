@@ -68,7 +68,7 @@ static int scenario(const char* rec_name, const char* wt_name, int reps) {
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? std::atoi(argv[1]) : 3;
     const char* cases[][2] = {{"own", "other"}, {"legacy", "own"}, {"null", "own"}, {"own", "legacy"},
-                              {"own", "null"}, {"legacy", "legacy"}};
+                              {"own", "null"}, {"legacy", "legacy"}, {"null", "legacy"}, {"null", "null"}};
     int worst = 0;
     for (auto& c : cases) {
         std::printf("scenario %s->%s\n", c[0], c[1]);

@@ -25,6 +25,12 @@ for s in ${STEPS:-pytest}; do
         iirburst) IIR_BURST=${BURST:-20} IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirburst 600 python -u tools/iir_ab.py ;;
         chanab) run chanab 600 python -u tools/chan_ab.py ;;
         chanburst) CHAN_BURST=${BURST:-40} run chanburst 600 python -u tools/chan_ab.py ;;
+        # libab_cfg<N>: alternating whole bench lines of the builds in LIBS (tools/libs_ab.sh)
+        libab_cfg*) CONFIGS=${s#libab_cfg} run "$s" 900 bash tools/libs_ab.sh ${TAG}_$s ;;
+        # proflib_cfg<N>: a kernel-trace / stats profile of the bench under every build in LIBS
+        proflib_cfg*) c=${s#proflib_cfg}; for lib in $LIBS; do b=$(basename $lib .so)
+                run "${s}_$b" 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_${s}_$b -o run -- \
+                    python tools/bench_lib.py $lib --config $c --steps 20 --warmup 5 --no-cpu --no-parity --no-dropin; done ;;
         fenceprobe) run fenceprobe 120 tools/_build/fence_probe 3 ;;
         copyprobe) run copyprobe 300 tools/_build/copy_shape_probe ;;
         fftslice) run fftslice 300 python -u tools/fft_slice_ab.py ;;
