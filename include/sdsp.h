@@ -204,6 +204,10 @@ SDSP_API int sdsp_fir_set_state(sdsp_fir* h, const void* hist, size_t phase);
 SDSP_API int sdsp_fir_frequency_response(const sdsp_fir* h, double f, double* re_im);
 SDSP_API int sdsp_fir_group_delay(const sdsp_fir* h, double f, double* delay);
 SDSP_API int sdsp_fir_synchronize(sdsp_fir* h);
+/* diagnostic (no reference counterpart): how many calls on this handle queued device work or moved
+   its delay line between host and device (kernel launches, async copies, history pulls / flushes);
+   per-sample calls on the host step leave it unchanged */
+SDSP_API unsigned long long sdsp_fir_device_ops(const sdsp_fir* h);
 
 /* ------------------------------------------------------------------------
  * Polyphase filterbank and interpolating FIR

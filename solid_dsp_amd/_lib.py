@@ -151,6 +151,7 @@ def _optional_sigs():
     vp, sz, i, d, dp, szp = C.c_void_p, C.c_size_t, C.c_int, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_size_t)
     vpp = C.POINTER(C.c_void_p)
     return {
+        "sdsp_fir_device_ops": (C.c_ulonglong, [C.c_void_p]),  # round 5 (older builds lack it)
         "sdsp_iir_create": (i, [vpp, i, vp, sz, vp, sz, i, i]),
         "sdsp_iir_decim_create": (i, [vpp, i, vp, sz, vp, sz, i, sz, i]),
         "sdsp_iir_interp_create": (i, [vpp, i, vp, sz, vp, sz, i, sz, i]),

@@ -111,9 +111,10 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // loaded last to first; 512 output rows stored last to first; 1024 each XCD walks the
 // even segments of its eighth, then the odd ones (a segment's halo row is then read
 // long after its neighbour's tail: from HBM, not as a hit on an in-flight L2 miss); 2097152 rows
-// loaded in row order (the product loads them in the first radix-4 stage's order); 4194304 the
-// twiddle-base tables requested after the rows; 8388608 no boundary / history code (timing only:
-// the first segment reads zeros before the stream and the history is not written);
+// loaded in the first radix-4 stage's order (the product: row order); 4194304 the
+// twiddle-base tables requested after the rows; 16777216 the rows issued exactly in the loop's
+// order (a scheduling barrier after each load); 33554432 the boundary segments as extra
+// workgroups of the interior launch (a branch at the kernel's entry);
 // ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
 // twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores; 16384
 // plain (not nontemporal) input loads; 32768 all six twiddle bases loaded (the round-3 form;
@@ -121,17 +122,18 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // kernel's shape); 262144 clock stamps (lab builds that define SDSP_OLS_STAMPS only: every 32nd
 // workgroup records s_memtime / s_memrealtime at entry and exit into g_ols_stamps, a buffer no
 // other code reads; the in-kernel clock of MI355X_MICROARCH.md "DVFS give-back" item 6).
-template <int ABL>
+template <int ABL, bool EDGE>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f2* __restrict__ hist,
                                                f2* __restrict__ new_hist, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
                                                long long n, int Lm1, int h2, f2* img, int t) {
     const int hi4 = t >> 4, lo4 = t & 15;
-    // the segment's window x[base, base + 4096) as a raw buffer: past the end of the stream
-    // (the last segment) loads return 0 and stores are dropped, so only a window that starts
-    // before the stream (base < 0: the first segments) needs the history path below
+    // the segment's window x[base, base + 4096) as a raw buffer.  EDGE (the boundary segments of a
+    // call, launched apart so that the interior kernel carries no boundary code: its presence
+    // alone cost the interior segments 1.9 %, profiles/r05/lab/r05e_olsburst.log): past the end of
+    // the stream loads return 0 and stores are dropped, rows before it come from the history
     const long long rem = n - base;
-    const int nrec = rem >= 4096 ? 32768 : (int)(8 * rem);
+    const int nrec = (!EDGE || rem >= 4096) ? 32768 : (int)(8 * rem);
     const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, nrec, kBufWord3);
     const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, nrec, kBufWord3);
     const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
@@ -156,39 +158,12 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
             tq[3] = tab(lo4, 12288), tq[4] = tab(lo4, 12544), tq[5] = tab(lo4, 12800);
         }
     };
-    if constexpr ((ABL & 4194304) == 0) load_tables();
     f2 v[16];
-    // The segment's rows, for every segment through the same loads (a window that starts before
-    // the stream reads zeros here, through an empty descriptor, and is completed below), in the
-    // order the first radix-4 stage consumes them (rows nb, 4 + nb, 8 + nb, 12 + nb for nb = 0..3:
-    // its first butterflies start after four rows have landed).  A branch around these loads
-    // would join with the boundary path before P1 and make the compiler wait for every row there.
-    const auto rxl = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, base < 0 ? 0 : nrec, kBufWord3);
-    if constexpr ((ABL & 524288) != 0) {
-        // 16-byte lanes: lane t = 2c + h loads columns (2c, 2c + 1) of rows k + 8h, then one DPP
-        // exchange per dword with its partner lane t ^ 1 gives it column t over the 16 rows
-        f4v q[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            q[k] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rxl, 16 * (t >> 1) + 16384 * (t & 1),
-                                                                                2048 * k, kLdAux));
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pair_exchange(f2{q[k].x, q[k].y}, f2{q[k].z, q[k].w}, v[k], v[8 + k]);
-    } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int r = (ABL & 256) ? 15 - i : (ABL & 2097152) ? i : 4 * (i & 3) + (i >> 2);
-            if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
-            else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
-            else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rxl, 8 * t, 2048 * r, kLdAux));
-        }
-    }
-    if constexpr ((ABL & 4194304) != 0) load_tables();  // lab: the tables after the rows
-    if ((ABL & 8388608) == 0 && base < 0) {
-        // the first segments: rows inside the stream again through rx, rows before it from the
-        // handle's history (the last Lm1 inputs, oldest first; positions before the history read
-        // as 0 through an out-of-range offset).  Waits for its loads before the join, so the
-        // interior path keeps its partial waits.
+    if constexpr (EDGE) {
+        // rows inside the stream through rx, rows before it from the handle's history (the last
+        // Lm1 inputs, oldest first; positions before the history read as 0 through an
+        // out-of-range offset)
+        load_tables();
         const auto rp = __builtin_amdgcn_make_buffer_rsrc((void*)hist, (short)0, 8 * Lm1, kBufWord3);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -200,7 +175,43 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
                 v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rp, e >= 0 ? (int)(8 * e) : 0x7ffffff0, 0, 0));
             }
         }
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        if (new_hist != nullptr) {
+            // the call's last segment: its window holds the last Lm1 inputs (halo >= Lm1), which
+            // become the history of the next call (ping-pong buffer: never the one read above)
+            const long long h0 = n - Lm1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const long long i = base + 256 * r + t - h0;
+                if (i >= 0 && i < Lm1) new_hist[i] = v[r];
+            }
+        }
+    } else {
+        if constexpr ((ABL & 4194304) == 0) load_tables();
+        // the rows in row order (the compiler interleaves them as 0, 4, 1, 5, 8, 12, 9, 13, ...):
+        // 2 % faster than the first radix-4 stage's order (0, 4, 8, 12, 1, 5, ...) and than either
+        // order enforced with scheduling barriers (profiles/r05/lab/r05h_olsburst.log,
+        // r05i_olsburst.log)
+        if constexpr ((ABL & 524288) != 0) {
+            // 16-byte lanes: lane t = 2c + h loads columns (2c, 2c + 1) of rows k + 8h, then one
+            // DPP exchange per dword with its partner lane t ^ 1 gives it column t over the rows
+            f4v q[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                q[k] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, 16 * (t >> 1) + 16384 * (t & 1),
+                                                                                    2048 * k, kLdAux));
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pair_exchange(f2{q[k].x, q[k].y}, f2{q[k].z, q[k].w}, v[k], v[8 + k]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r = (ABL & 256) ? 15 - i : (ABL & 2097152) ? 4 * (i & 3) + (i >> 2) : i;
+                if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
+                else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
+                else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, kLdAux));
+                if constexpr ((ABL & 16777216) != 0) __builtin_amdgcn_sched_barrier(0);  // lab: issue in this order
+            }
+        }
+        if constexpr ((ABL & 4194304) != 0) load_tables();  // lab: the tables after the rows
     }
     if constexpr ((ABL & 4) && (ABL & 131072)) {
         // HBM-only with the NCO kernel's lane shape: the segment as eight 4 KB rows of 16-byte
@@ -247,16 +258,6 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         Da[0] = f2{b1.z, b1.w}, Da[1] = f2{b2.x, b2.y}, Da[2] = f2{b2.z, b2.w};
         Eb[0] = f2{e0.x, e0.y}, Eb[1] = f2{e0.z, e0.w}, Eb[2] = f2{e1.x, e1.y};
         Fa[0] = f2{e1.z, e1.w}, Fa[1] = f2{e2.x, e2.y}, Fa[2] = f2{e2.z, e2.w};
-    }
-    if ((ABL & 8388608) == 0 && new_hist != nullptr) {
-        // the call's last segment: its window holds the last Lm1 inputs (halo >= Lm1), which
-        // become the history of the next call (ping-pong buffer: never the one read above)
-        const long long h0 = n - Lm1;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const long long i = base + 256 * r + t - h0;
-            if (i >= 0 && i < Lm1) new_hist[i] = v[r];
-        }
     }
     f2* col = img + t + (t >> 4);  // (r, t) at col[r * kRow]
 
@@ -327,7 +328,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     // nontemporal stores (3.14 -> 3.08 ms on cfg2, in-process A/B); rows < h2 wrap and are dropped,
     // positions past the stream fall outside the descriptor (dropped)
     constexpr int kStAux = (ABL & 8192) ? 16 : (ABL & 128) ? 0 : 2;  // 16: write-through (sc1), lab
-    if constexpr ((ABL & 524288) != 0) {
+    if constexpr ((ABL & 524288) != 0 && !EDGE) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             f2 a, b;
@@ -350,27 +351,50 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
 __device__ unsigned long long g_ols_stamps[4 * 8192];
 #endif
 
-template <int ABL>
+// Interior segments [lo, hi) of every channel (whole window inside the stream): workgroup b
+// runs on XCD b % 8 and takes segment lo + (b % 8) q + b / 8, so each XCD streams one contiguous
+// eighth of the call in order.  EDGE: the boundary segments [0, lo) and [hi, nseg) (block b takes
+// segment b < lo ? b : hi + b - lo), the last one writing the next history (new_hist).
+template <int ABL, bool EDGE>
 __global__ void __launch_bounds__(256, 4)
 fir_ols_os_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, f2* __restrict__ new_hist,
                   const float4* __restrict__ Hs, const float4* __restrict__ tb, f2* __restrict__ y, long long n,
-                  long long nseg, long long q, int h2, int Lm1) {
+                  long long lo, long long hi, long long q, long long nseg, int h2, int Lm1) {
     __shared__ __attribute__((aligned(16))) f2 img[16 * kRow];
-    const int xc = blockIdx.x & 7;
-    long long j = blockIdx.x >> 3;
-    if constexpr ((ABL & 1024) != 0) j = j < (q + 1) / 2 ? 2 * j : 2 * (j - (q + 1) / 2) + 1;
-    const long long seg = (long long)xc * q + j;
-    const long long xe = (long long)(xc + 1) * q;
-    if (seg >= (xe < nseg ? xe : nseg)) return;  // uniform over the workgroup
+    long long seg;
+    if constexpr (!EDGE && (ABL & 33554432) != 0) {
+        // lab: the boundary segments as extra workgroups past the interior grid, on their own
+        // code path (one launch instead of two)
+        const long long nb = 8 * q;
+        if ((long long)blockIdx.x >= nb) {
+            const long long b = (long long)blockIdx.x - nb;
+            const long long sg = b < lo ? b : hi + (b - lo);
+            const long long c = blockIdx.y;
+            ols_os_segment<0, true>(x + c * n, hist + c * Lm1,
+                                    (new_hist != nullptr && sg == nseg - 1) ? new_hist + c * Lm1 : nullptr, Hs, tb,
+                                    y + c * n, sg * (4096 - 256 * h2) - 256 * h2, n, Lm1, h2, img, threadIdx.x);
+            return;
+        }
+    }
+    if constexpr (EDGE) {
+        seg = (long long)blockIdx.x < lo ? (long long)blockIdx.x : hi + ((long long)blockIdx.x - lo);
+    } else {
+        const int xc = blockIdx.x & 7;
+        long long j = blockIdx.x >> 3;
+        if constexpr ((ABL & 1024) != 0) j = j < (q + 1) / 2 ? 2 * j : 2 * (j - (q + 1) / 2) + 1;
+        seg = lo + (long long)xc * q + j;
+        const long long xe = lo + (long long)(xc + 1) * q;
+        if (seg >= (xe < hi ? xe : hi)) return;  // uniform over the workgroup
+    }
     const int V = 4096 - 256 * h2;
     const long long ch = blockIdx.y;
 #ifdef SDSP_OLS_STAMPS
     unsigned long long m0 = 0, r0 = 0;
     if constexpr ((ABL & 262144) != 0) m0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    ols_os_segment<ABL>(x + ch * n, hist + ch * Lm1,
-                        (new_hist != nullptr && seg == nseg - 1) ? new_hist + ch * Lm1 : nullptr, Hs, tb, y + ch * n,
-                        seg * V - 256 * h2, n, Lm1, h2, img, threadIdx.x);
+    ols_os_segment<ABL, EDGE>(x + ch * n, hist + ch * Lm1,
+                              (EDGE && new_hist != nullptr && seg == nseg - 1) ? new_hist + ch * Lm1 : nullptr, Hs,
+                              tb, y + ch * n, seg * V - 256 * h2, n, Lm1, h2, img, threadIdx.x);
 #ifdef SDSP_OLS_STAMPS
     if constexpr ((ABL & 262144) != 0) {
         const unsigned long long m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -382,9 +406,9 @@ fir_ols_os_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, f2* __r
 #endif
 }
 
-// every segment of every channel in one grid (the first segments read the history, the last
-// one is bounded by the stream and, with new_hist, writes the next call's history); ABL as
-// above (0 = the product kernel)
+// every segment of every channel: the boundary segments (and the next history) in one small
+// launch, the interior ones in the XCD-ordered grid; ABL as above for the interior kernel (0 = the
+// product kernel)
 template <int ABL>
 hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
                                int Lm1, size_t channels, hipStream_t s, size_t dyn_lds) {
@@ -393,11 +417,26 @@ hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, const void* hist
     if (h2 < 1 || h2 > 15 || Lm1 > 256 * h2) return hipErrorInvalidValue;
     const long long V = 4096 - 256 * h2;
     const long long nseg = ((long long)n + V - 1) / V;
-    const long long q = (nseg + 7) / 8;
-    const dim3 grid((unsigned)(8 * q), (unsigned)channels);
-    hipLaunchKernelGGL(fir_ols_os_kernel<ABL>, grid, dim3(256), dyn_lds, s, (const f2*)x, (const f2*)hist,
-                       (f2*)new_hist, (const float4*)p.d_pkt, (const float4*)p.d_ostab, (f2*)y, (long long)n, nseg, q,
-                       h2, Lm1);
+    long long lo, hi;
+    ols_interior_range((long long)n, h2, &lo, &hi);
+    if (hi > nseg - 1) hi = nseg - 1;  // the last segment always runs in the boundary launch (history)
+    if (hi < lo) hi = lo;
+    const long long nedge = lo + (nseg - hi);
+    const long long q = (hi - lo + 7) / 8;
+    if constexpr ((ABL & 33554432) != 0) {  // lab: one launch, the boundary segments past the grid
+        hipLaunchKernelGGL((fir_ols_os_kernel<ABL, false>), dim3((unsigned)(8 * q + nedge), (unsigned)channels),
+                           dim3(256), dyn_lds, s, (const f2*)x, (const f2*)hist, (f2*)new_hist, (const float4*)p.d_pkt,
+                           (const float4*)p.d_ostab, (f2*)y, (long long)n, lo, hi, q, nseg, h2, Lm1);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((fir_ols_os_kernel<0, true>), dim3((unsigned)nedge, (unsigned)channels), dim3(256), 0, s,
+                       (const f2*)x, (const f2*)hist, (f2*)new_hist, (const float4*)p.d_pkt, (const float4*)p.d_ostab,
+                       (f2*)y, (long long)n, lo, hi, 0LL, nseg, h2, Lm1);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || hi <= lo) return e;
+    hipLaunchKernelGGL((fir_ols_os_kernel<ABL, false>), dim3((unsigned)(8 * q), (unsigned)channels), dim3(256), dyn_lds,
+                       s, (const f2*)x, (const f2*)hist, (f2*)nullptr, (const float4*)p.d_pkt, (const float4*)p.d_ostab,
+                       (f2*)y, (long long)n, lo, hi, q, nseg, h2, Lm1);
     return hipGetLastError();
 }
 

@@ -192,7 +192,8 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // kernels are LAB = 0): ablations 1 no zero-state run, 2 no scan, 4 no correction, 8 no HBM
 // loads, 16 no HBM stores; variants 32 plain (not nontemporal) loads, 64 plain stores, 128
 // nontemporal stores (the round-3 product; the product's interior stores are write-through), 256
-// the scalar correction (the round-3 arithmetic; real f32), 512 every scan level (the round-4 scan)
+// the scalar correction (the round-3 arithmetic; real f32), 512 every scan level (the round-4 scan),
+// 1024 compiled for one rate without exact carries
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -203,6 +204,11 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     constexpr int D = ND ? ND : 2 * S;
     constexpr int B = ws_chunk<I, CB>::B;
     constexpr bool RERUN = FORM == 1, PF = FORM != 2;
+    // LAB 1024: the warm-up scan at one rate only (Mi = Md = 1, no exact-carry passes) compiled
+    // without the other paths (lab: what their code costs when it never runs)
+    if constexpr ((LAB & 1024) != 0) {
+        Mi = 1, Md = 1, cin = nullptr, gagg = nullptr;
+    }
     // real f32: the correction in packed math over sample pairs (Cr in the [B/2][D][2] layout,
     // runtime_iir.cpp scan_tables); LAB 256: the scalar form over the same layout
     constexpr bool kPairCr = std::is_same<I, float>::value && std::is_same<C, float>::value;  // the layout

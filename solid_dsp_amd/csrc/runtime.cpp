@@ -85,6 +85,7 @@ using namespace sdsp;
 // ===========================================================================
 struct sdsp_fir {
     int dtype = 0, device = 0, cus = 256;
+    mutable unsigned long long device_ops = 0;  // sdsp_fir_device_ops
     size_t L = 0, M = 1, channels = 1;
     std::vector<unsigned char> taps;   // original order (host copy for coefficients / design queries)
     std::vector<unsigned char> scale;  // one Coef
@@ -397,6 +398,7 @@ int host_pull(sdsp_fir* h) {
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     const size_t lm1 = h->L - 1, sb = sample_bytes(h->dtype);
     h->hbuf.resize(2 * lm1 * sb);
+    ++h->device_ops;
     if (lm1) {
         SDSP_TRY(hipMemcpy(h->hbuf.data(), h->d_hist[h->cur].p, lm1 * sb, hipMemcpyDeviceToHost), "pull history");
         std::memcpy(h->hbuf.data() + lm1 * sb, h->hbuf.data(), lm1 * sb);
@@ -412,6 +414,7 @@ int host_pull(sdsp_fir* h) {
 int host_flush(const sdsp_fir* hc) {
     sdsp_fir* h = const_cast<sdsp_fir*>(hc);
     if (!h->dev_stale) return SDSP_OK;
+    ++h->device_ops;
     const size_t lm1 = h->L - 1, sb = sample_bytes(h->dtype);
     if (lm1)
         SDSP_TRY(hipMemcpy(h->d_hist[h->cur].p, h->hbuf.data() + h->hpos * sb, lm1 * sb, hipMemcpyHostToDevice),
@@ -463,6 +466,7 @@ int host_run(sdsp_fir* h, const unsigned char* in, size_t n, unsigned char* out,
 // the phase emits and `want` is set) lands in host-mapped memory
 int fir_step_device(sdsp_fir* h, const void* sample, void* out, size_t* n_out, bool want) {
     SDSP_TRY(h->fence.wait(), "wait for queued work");
+    ++h->device_ops;
     int st = host_flush(h);
     if (st) return st;
     if (!h->step_out.host) {
@@ -673,6 +677,7 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
     }
     int hst = host_flush(h);
     if (hst) return hst;
+    ++h->device_ops;
     h->host_valid = false;  // the input is device-resident: the host window is re-read when needed
     // work queued on another stream (the fence) reads or writes the history this launch uses
     SDSP_TRY(h->fence.order_before(s), "order after queued work");
@@ -748,6 +753,7 @@ int sdsp_decim_write(sdsp_fir* h, const void* samples, size_t n) {
     int hst = host_flush(h);
     if (hst) return hst;
     const size_t sb = sample_bytes(h->dtype);
+    ++h->device_ops;
     SDSP_TRY(h->stage_in.ensure(h->channels * n * sb), "stage in");
     SDSP_TRY(hipMemcpyAsync(h->stage_in.p, samples, h->channels * n * sb, hipMemcpyHostToDevice, h->stream), "H2D");
     SDSP_TRY(launch_hist_update(h->dtype, h->stage_in.p, h->d_hist[h->cur].p, h->d_hist[h->cur ^ 1].p, n,
@@ -824,6 +830,8 @@ int sdsp_fir_group_delay(const sdsp_fir* h, double f, double* delay) {
     *delay = d;
     return SDSP_OK;
 }
+
+unsigned long long sdsp_fir_device_ops(const sdsp_fir* h) { return h ? h->device_ops : 0; }
 
 int sdsp_fir_synchronize(sdsp_fir* h) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
