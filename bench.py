@@ -221,8 +221,8 @@ class Cfg2FIR(StreamShard):
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (f32 taps x complex-f32 samples, f32 accumulate)"
         self.kernel = {"fft": "fir_ols_os_kernel (one-shot XCD-ordered packed-FP32 overlap-save N=4096, one segment "
-                              "per workgroup, 4 workgroups/CU; every segment of the call, the history update "
-                              "included, in one launch)",
+                              "per workgroup, 4 workgroups/CU) + fir_ols_os_kernel<0, true> (the 2 boundary "
+                              "segments and the next history, a second launch)",
                        "exact": "fir_direct_kernel<EXACT>",
                        "fma": "fir_direct_kernel<FMA>"}[args.algo]
         self.workload = (f"cfg2: 256-tap crcf FIR, firdes_kaiser(256, 0.1, 80), scale 0.2, 2^{args.log2n} samples "

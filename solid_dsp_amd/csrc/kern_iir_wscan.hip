@@ -55,6 +55,33 @@ template <typename T> __device__ __forceinline__ cpx<T> shfl_up_v(cpx<T> v, int 
     return {__shfl_up(v.re, d), __shfl_up(v.im, d)};
 }
 template <typename T> __device__ __forceinline__ T readlane_v(T v, int l) { return __shfl(v, l); }
+
+// the whole-wave shift by one lane (lane l gets lane l - 1's value; lane 0's result is not used)
+// as DPP moves (wave_shr:1) instead of LDS-routed ds_bpermute shuffles: a few cycles of latency
+// instead of an LDS round trip on the scan's dependent chain.  Eight dwords per statement, one
+// s_nop 1 for the DPP read-after-VALU-write hazard of values computed just before.
+[[maybe_unused]] __device__ __forceinline__ void shfl_up1_x8(const float (&a)[8], float (&r)[8]) {
+    asm("s_nop 1\n\t"
+        "v_mov_b32_dpp %0, %8 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %1, %9 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %2, %10 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %3, %11 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %4, %12 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %5, %13 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %6, %14 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_mov_b32_dpp %7, %15 wave_shr:1 row_mask:0xf bank_mask:0xf"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]));
+}
+// lane l - 1's values of an I[D] state (the DPP form for real f32 with D = 8, else shuffles)
+template <bool DPP, int D, typename I> __device__ __forceinline__ void shfl_up1_state(const I (&a)[D], I (&r)[D]) {
+    if constexpr (DPP && D == 8 && std::is_same<I, float>::value) {
+        shfl_up1_x8(a, r);
+    } else {
+#pragma unroll
+        for (int d = 0; d < D; ++d) r[d] = shfl_up_v(a[d], 1);
+    }
+}
 template <typename T> __device__ __forceinline__ cpx<T> readlane_v(cpx<T> v, int l) {
     return {__shfl(v.re, l), __shfl(v.im, l)};
 }
@@ -193,7 +220,8 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // loads, 16 no HBM stores; variants 32 plain (not nontemporal) loads, 64 plain stores, 128
 // nontemporal stores (the round-3 product; the product's interior stores are write-through), 256
 // the scalar correction (the round-3 arithmetic; real f32), 512 every scan level (the round-4 scan),
-// 1024 compiled for one rate without exact carries
+// 1024 compiled for one rate without exact carries, 2048 the lane shifts by one as DPP wave_shr
+// moves (real f32, D = 8)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__(kWsThreads)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -353,8 +381,12 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             if (k >= nlev) break;  // the terms of lanes >= 2^nlev back have decayed (see nlev)
             const int off = 1 << k;
             I prev[D], a[D];
+            if (k == 0) {
+                shfl_up1_state<(LAB & 2048) != 0>(s, prev);
+            } else {
 #pragma unroll
-            for (int d = 0; d < D; ++d) prev[d] = shfl_up_v(s[d], off);
+                for (int d = 0; d < D; ++d) prev[d] = shfl_up_v(s[d], off);
+            }
             sys_matvec<ND>(sP + k * D * D, prev, a);
             if (lane >= off) {
 #pragma unroll
@@ -362,10 +394,11 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
             }
         }
         I init[D];
+        {
+            I up[D];
+            shfl_up1_state<(LAB & 2048) != 0>(s, up);
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const I up = shfl_up_v(s[d], 1);
-            init[d] = lane == 0 ? carry[d] : up;
+            for (int d = 0; d < D; ++d) init[d] = lane == 0 ? carry[d] : up[d];
         }
 #pragma unroll
         for (int d = 0; d < D; ++d) carry[d] = readlane_v(s[d], 63);

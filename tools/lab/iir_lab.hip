@@ -38,6 +38,7 @@ static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw)
         case 280: return lab_cfg3<CB, 280>(a, st, tpw);
         case 512: return lab_cfg3<CB, 512>(a, st, tpw);
         case 1024: return lab_cfg3<CB, 1024>(a, st, tpw);
+        case 2048: return lab_cfg3<CB, 2048>(a, st, tpw);
         default: return lab_cfg3<CB, 0>(a, st, tpw);
     }
 }

@@ -37,6 +37,8 @@ def main():
     p.add_argument("--write", required=True)
     p.add_argument("--algorithmic-bytes", type=float, default=None)
     p.add_argument("--out", required=True)
+    p.add_argument("--label", default=None, help="kernel name to record (default: --kernel); bench.py matches "
+                                                   "it as a prefix of the kernel it launches")
     a = p.parse_args()
     fk = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     wk = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
@@ -45,7 +47,7 @@ def main():
     fetch_b = 2.0 * statistics.median(fk) * 1024.0
     write_b = statistics.median(wk) * 1024.0
     out = {
-        "config": a.config, "kernel": a.kernel, "log2n": a.log2n, "algo": a.algo,
+        "config": a.config, "kernel": a.label or a.kernel, "dispatch_match": a.kernel, "log2n": a.log2n, "algo": a.algo,
         "dispatches": {"fetch": len(fk), "write": len(wk)},
         "fetch_size_kib_median": statistics.median(fk), "write_size_kib_median": statistics.median(wk),
         "hbm_read_bytes_per_launch": fetch_b, "hbm_write_bytes_per_launch": write_b,
