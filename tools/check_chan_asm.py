@@ -21,7 +21,24 @@ import subprocess
 import sys
 import tempfile
 
-LLVM = "/opt/rocm/llvm/bin"
+def _llvm_bin():
+    """the ROCm LLVM tools (llvm-objcopy, clang-offload-bundler, llvm-objdump): from ROCM_PATH,
+    else next to HIPCC's ROCm, else /opt/rocm (the build must not assume one prefix)"""
+    cands = []
+    if os.environ.get("ROCM_PATH"):
+        cands.append(os.path.join(os.environ["ROCM_PATH"], "llvm", "bin"))
+    hipcc = os.environ.get("HIPCC")
+    if hipcc:
+        cands.append(os.path.join(os.path.dirname(os.path.dirname(os.path.realpath(hipcc))), "llvm", "bin"))
+    cands.append("/opt/rocm/llvm/bin")
+    for c in cands:
+        if all(os.path.exists(os.path.join(c, t)) for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-objdump")):
+            return c
+    sys.exit("check_chan_asm: llvm-objcopy / clang-offload-bundler / llvm-objdump not found under " + ", ".join(cands) +
+             " (set ROCM_PATH)")
+
+
+LLVM = _llvm_bin()
 KERNEL = re.compile(r"^([0-9a-f]+) <(_Z\w*chan1024_kernelILi(\d)ELi1024ELb1ELi8ELi0EE\w*)>:$")
 INSN = re.compile(r"^\s+([a-z_0-9]+)(.*?)\s*//\s*([0-9A-F]+):")
 TARGET = re.compile(r"<\w+\+0x([0-9a-f]+)>")
