@@ -658,7 +658,7 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + ib), (short)0, ok ? 0x7fffffff : 0, 0x00020000);
 #pragma unroll
         for (int k = k0; k < k1; ++k)
-            v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, LA));
+            v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, LA & 3));
     };
     long long grp = blockIdx.x;
     if (grp >= ngroups) return;  // uniform
@@ -686,7 +686,8 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         // scratch too): cfg8 2.09 ms with all sixteen, 1.79 with eight, 1.90 with four
         const long long nxt = grp + gridDim.x;
         load(nxt, 0, kPre, nxt < ngroups);
-        fft1024_wave_lds(sbuf + w * kPassBuf, stw, L);
+        // LA & 8 (lab only): the pass's skeleton -- loads, staging, twiddle and stores, no FFT
+        if constexpr ((LA & 8) == 0) fft1024_wave_lds(sbuf + w * kPassBuf, stw, L);
         __syncthreads();
         load(nxt, kPre, 16, nxt < ngroups);
         const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ob), (short)0, 0x7fffffff, 0x00020000);

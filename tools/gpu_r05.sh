@@ -31,6 +31,10 @@ for s in ${STEPS:-pytest}; do
         proflib_cfg*) c=${s#proflib_cfg}; for lib in $LIBS; do b=$(basename $lib .so)
                 run "${s}_$b" 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_${s}_$b -o run -- \
                     python tools/bench_lib.py $lib --config $c --steps 20 --warmup 5 --no-cpu --no-parity --no-dropin; done ;;
+        # fftprof: the cfg8 pass kernels per case in FFT_CASES (kernel trace), then the stride probe
+        fftprof) FFT_ROUNDS=${FROUNDS:-5} run fftprof 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                     -d gpurun_out/${TAG}_fftprof -o run -- python -u tools/fft_lab.py
+                 run strideprobe 200 tools/_build/stride_probe ;;
         fenceprobe) run fenceprobe 120 tools/_build/fence_probe 3 ;;
         copyprobe) run copyprobe 300 tools/_build/copy_shape_probe ;;
         fftslice) run fftslice 300 python -u tools/fft_slice_ab.py ;;

@@ -13,10 +13,9 @@ namespace sdsp {
 
 static int g_iir_lab = 0;
 
-// LAB bit 4096 (lab only): the FORM 2 kernel (no register prefetch of the next tile)
 template <int CB, int LAB>
 static hipError_t lab_cfg3(const IirArgs& a, hipStream_t st, int tpw) {
-    return launch_wscan_t<float, float, 4, CB, (LAB & 4096) ? 2 : 0, 0, (LAB & ~4096)>(a, st, tpw);
+    return launch_wscan_t<float, float, 4, CB, 0, 0, LAB>(a, st, tpw);
 }
 
 template <int CB>
@@ -40,8 +39,9 @@ static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw)
         case 512: return lab_cfg3<CB, 512>(a, st, tpw);
         case 1024: return lab_cfg3<CB, 1024>(a, st, tpw);
         case 2048: return lab_cfg3<CB, 2048>(a, st, tpw);
-        case 4096: return lab_cfg3<CB, 4096>(a, st, tpw);
-        case 6144: return lab_cfg3<CB, 6144>(a, st, tpw);
+        // codes past the LAB bits (the value's low 12 bits): 3072 = the FORM 2 kernel (no register
+        // prefetch) with the DPP lane shifts (LAB 2048: 116 VGPRs, 4 waves per SIMD)
+        case 3072: return launch_wscan_t<float, float, 4, CB, 2, 0, 2048>(a, st, tpw);
         default: return lab_cfg3<CB, 0>(a, st, tpw);
     }
 }
