@@ -613,7 +613,9 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 // contiguous runs.  Same arithmetic, element order and twiddles as
 // fft1024_pass_kernel<INV, TW, TPB> (bit-identical).  PRE: next-group loads issued before
 // the FFT (the rest after it).
-// LA / SA: the loads' / stores' cache policy (0 default, 2 nontemporal; lab variants)
+// LA / SA: the loads' / stores' cache policy (0 default, 2 nontemporal; lab variants), LA & 8
+// the skeleton without the FFT, LA / SA & 16 16-byte lanes on the strided side, LA & 32
+// XCD-ordered groups (lab)
 template <bool INV, bool TW, bool CFAST, bool OFAST, int TPB = 16, int PRE = 8, int LA = 0, int SA = 0>
 __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* __restrict__ y,
                                                   const cf* __restrict__ tw, const cf* __restrict__ twx,
@@ -647,7 +649,14 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
     const unsigned in_k = (unsigned)(cfast ? 64 * Si : S1) * 8u;
     const unsigned out_lane = (unsigned)(ofast ? ((t & (TPB - 1)) + (long long)(t >> kLog) * So) : (long long)t * So) * 8u;
     const unsigned out_k = (unsigned)(ofast ? 64 * So : T1) * 8u;
+    // LA / SA & 16 (lab only): 16-byte lanes on the strided side, lane t holding columns
+    // 2 (t & 7) and 2 (t & 7) + 1 of rows (t >> 3) + 128 m, m = k / 2 (the stride probe's lane shape)
+    constexpr bool wide_in = (LA & 16) != 0 && cfast, wide_out = (SA & 16) != 0 && ofast;
+    const unsigned in_lane16 = (unsigned)(2 * (t & 7) + (long long)(t >> 3) * Si) * 8u, in_k16 = (unsigned)(128 * Si) * 8u;
+    const unsigned out_lane16 = (unsigned)(2 * (t & 7) + (long long)(t >> 3) * So) * 8u, out_k16 = (unsigned)(128 * So) * 8u;
     typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    typedef float f4v __attribute__((ext_vector_type(4)));
     cf v[16];
     // past the last group (ok false): an empty descriptor, so the loads return zeros without touching
     // memory and every path issues the same loads -- no branch around them, whose merge would make
@@ -656,55 +665,107 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         long long ib, ob, g0;
         bases(ok ? grp : 0, ib, ob, g0);
         const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + ib), (short)0, ok ? 0x7fffffff : 0, 0x00020000);
+        if constexpr (wide_in) {
 #pragma unroll
-        for (int k = k0; k < k1; ++k)
-            v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, LA & 3));
+            for (int m = k0 / 2; m < k1 / 2; ++m) {
+                const f4v q = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rx, in_lane16, m * in_k16, LA & 3));
+                v[2 * m] = cf{q.x, q.y}, v[2 * m + 1] = cf{q.z, q.w};
+            }
+        } else {
+#pragma unroll
+            for (int k = k0; k < k1; ++k)
+                v[k] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(rx, in_lane, k * in_k, LA & 3));
+        }
+    };
+    // LA & 32 (lab): XCD-ordered groups, workgroup b on XCD b % 8 walking that XCD's contiguous
+    // eighth (when the grid is a whole number of workgroups per XCD); the product form names
+    // gridDim / ngroups directly
+    auto next_of = [&](long long g) -> long long {
+        if constexpr ((LA & 32) != 0) return g + ((gridDim.x & 7) == 0 ? gridDim.x >> 3 : gridDim.x);
+        else return g + gridDim.x;
+    };
+    auto last = [&]() -> long long {
+        if constexpr ((LA & 32) != 0) {
+            const long long e = ((ngroups + 7) / 8) * ((blockIdx.x & 7) + 1);
+            return (gridDim.x & 7) == 0 && e < ngroups ? e : ngroups;
+        } else {
+            return ngroups;
+        }
     };
     long long grp = blockIdx.x;
-    if (grp >= ngroups) return;  // uniform
+    if constexpr ((LA & 32) != 0)
+        if ((gridDim.x & 7) == 0) grp = ((ngroups + 7) / 8) * (blockIdx.x & 7) + (blockIdx.x >> 3);
+    if (grp >= last()) return;  // uniform
     load(grp, 0, 16);
     for (;;) {
         // stage the group's columns (waits for its loads: the previous stores may stay in flight)
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int e = t + kT * k;
-            const int c = cfast ? (e & (TPB - 1)) : (e >> 10), i = cfast ? (e >> kLog) : (e & 1023);
+            int c = cfast ? (e & (TPB - 1)) : (e >> 10), i = cfast ? (e >> kLog) : (e & 1023);
+            if constexpr (wide_in) c = 2 * (t & 7) + (k & 1), i = (t >> 3) + 128 * (k >> 1);
             sbuf[c * kPassBuf + i] = INV ? cf{v[k].re, -v[k].im} : v[k];
         }
         long long ib, ob, g0;
         bases(grp, ib, ob, g0);
-        cf tbase = cf{1.0f, 0.0f};
+        cf tbase = cf{1.0f, 0.0f}, tbase1 = cf{1.0f, 0.0f};
         if constexpr (TW) {
             if (t < TPB * 16) ktab[t] = twx_at(64 * (g0 + (t >> 4)) * (long long)(t & 15));
-            if (ofast) tbase = twx_at((g0 + (t & (TPB - 1))) * (long long)(t >> kLog));
+            if constexpr (wide_out) {
+                tbase = twx_at((g0 + 2 * (t & 7)) * (long long)(t >> 3));
+                tbase1 = twx_at((g0 + 2 * (t & 7) + 1) * (long long)(t >> 3));
+            } else if (ofast) {
+                tbase = twx_at((g0 + (t & (TPB - 1))) * (long long)(t >> kLog));
+            }
         }
         asm volatile("" : "+v"(tbase.re), "+v"(tbase.im));  // formed here, before the next group's loads
+        if constexpr (wide_out) asm volatile("" : "+v"(tbase1.re), "+v"(tbase1.im));
         __syncthreads();
         // the next group's loads: half in flight across this group's FFT, half across its
         // stores.  Holding more of them through the FFT makes it spill (1024 threads: 128
         // VGPRs), and every scratch reload waits for all outstanding loads (vmcnt counts
         // scratch too): cfg8 2.09 ms with all sixteen, 1.79 with eight, 1.90 with four
-        const long long nxt = grp + gridDim.x;
-        load(nxt, 0, kPre, nxt < ngroups);
+        const long long nxt = next_of(grp);
+        load(nxt, 0, kPre, nxt < last());
         // LA & 8 (lab only): the pass's skeleton -- loads, staging, twiddle and stores, no FFT
         if constexpr ((LA & 8) == 0) fft1024_wave_lds(sbuf + w * kPassBuf, stw, L);
         __syncthreads();
-        load(nxt, kPre, 16, nxt < ngroups);
+        load(nxt, kPre, 16, nxt < last());
         const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ob), (short)0, 0x7fffffff, 0x00020000);
+        if constexpr (wide_out) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int e = t + kT * k;
-            const int c = ofast ? (e & (TPB - 1)) : (e >> 10), i = ofast ? (e >> kLog) : (e & 1023);
-            cf r = sbuf[c * kPassBuf + i];
-            if (INV) r.im = -r.im;
-            if constexpr (TW) {
-                cf wv = ofast ? cmul(tbase, ktab[c * 16 + k]) : twx_at((g0 + c) * (long long)i);
-                if (INV) wv.im = -wv.im;
-                r = cmul(r, wv);
+            for (int m = 0; m < 8; ++m) {
+                cf r[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const int c = 2 * (t & 7) + j, i = (t >> 3) + 128 * m;
+                    r[j] = sbuf[c * kPassBuf + i];
+                    if (INV) r[j].im = -r[j].im;
+                    if constexpr (TW) {
+                        cf wv = cmul(j ? tbase1 : tbase, ktab[c * 16 + 2 * m]);
+                        if (INV) wv.im = -wv.im;
+                        r[j] = cmul(r[j], wv);
+                    }
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, f4v{r[0].re, r[0].im, r[1].re, r[1].im}), ry,
+                                                       out_lane16, m * out_k16, SA & 3);
             }
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, r), ry, out_lane, k * out_k, SA);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int e = t + kT * k;
+                const int c = ofast ? (e & (TPB - 1)) : (e >> 10), i = ofast ? (e >> kLog) : (e & 1023);
+                cf r = sbuf[c * kPassBuf + i];
+                if (INV) r.im = -r.im;
+                if constexpr (TW) {
+                    cf wv = ofast ? cmul(tbase, ktab[c * 16 + k]) : twx_at((g0 + c) * (long long)i);
+                    if (INV) wv.im = -wv.im;
+                    r = cmul(r, wv);
+                }
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, r), ry, out_lane, k * out_k, SA & 3);
+            }
         }
-        if (nxt >= ngroups) break;
+        if (nxt >= last()) break;
         grp = nxt;
         __syncthreads();  // every read of sbuf / ktab done before the next group is staged
     }

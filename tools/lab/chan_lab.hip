@@ -13,16 +13,27 @@ namespace sdsp {
 
 static int g_chan_lab = 0;
 static int g_fft_policy = 0;  // 4-step L = 1024 passes: bit 0 nontemporal loads, bit 1 nontemporal stores,
-                              // bit 2 no inter-pass twiddle (ablation)
+                              // bit 2 no inter-pass twiddle (ablation), 8 the pass skeleton
+                              // (loads, staging, twiddle, stores; no FFT), 16 / 32 16-byte
+                              // lanes on the strided side of the loads / stores, 64 XCD-ordered
+                              // groups
 
 bool try_launch_fft1024_pass(const FftPass& p_, hipStream_t s, hipError_t* err) {
     FftPass p = p_;
     if (g_fft_policy & 4) p.Ntw = 0;  // ablation: the column pass without its inter-pass twiddle (wrong results)
-    switch (g_fft_policy & 3) {
+    switch (g_fft_policy & 123) {
         case 1: return try_launch_fft1024_pass_t<2, 0>(p, s, err);
         case 2: return try_launch_fft1024_pass_t<0, 2>(p, s, err);
         case 3: return try_launch_fft1024_pass_t<2, 2>(p, s, err);
         case 8: return try_launch_fft1024_pass_t<8, 0>(p, s, err);  // skeleton: no FFT (timing only)
+        case 16: return try_launch_fft1024_pass_t<16, 0>(p, s, err);
+        case 32: return try_launch_fft1024_pass_t<0, 16>(p, s, err);
+        case 48: return try_launch_fft1024_pass_t<16, 16>(p, s, err);
+        case 56: return try_launch_fft1024_pass_t<24, 16>(p, s, err);
+        case 64: return try_launch_fft1024_pass_t<32, 0>(p, s, err);
+        case 72: return try_launch_fft1024_pass_t<40, 0>(p, s, err);
+        case 112: return try_launch_fft1024_pass_t<48, 16>(p, s, err);
+        case 120: return try_launch_fft1024_pass_t<56, 16>(p, s, err);
         default: return try_launch_fft1024_pass_t<0, 0>(p, s, err);
     }
 }
@@ -51,4 +62,4 @@ extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_chan_ablatio
     sdsp::g_chan_lab = (v & 7) | ((v >> 2) & 24) | ((v & 8) ? 32 : 0) | ((v & 16) ? 64 : 0) | (v & ~127);
 }
 
-extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_fft_policy(int v) { sdsp::g_fft_policy = v & 7; }
+extern "C" __attribute__((visibility("default"))) void sdsp_lab_set_fft_policy(int v) { sdsp::g_fft_policy = v & 127; }
