@@ -713,7 +713,7 @@ class Cfg8FFT:
         # plan makes two passes, so its floor is 2x this
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (complex-f32 butterflies, f64-derived twiddles)"
-        self.kernel = "fft1024_pipe_kernel x2 (four-step 1024 x 1024 on the wave-level register FFT, 16 transforms per step of a persistent, load-pipelined workgroup per CU)"
+        self.kernel = "fft1024_pipe_kernel x2 (four-step 1024 x 1024 on the wave-level register FFT, 16 transforms per step of a persistent, load-pipelined workgroup per CU; the column pass loads its strided side in 16-byte lanes)"
         self.parity_check = "rel_rms of transform 0 vs numpy f64 (tolerance 5e-6)"
         self.workload = f"cfg8: {self.batch} x 2^20-point forward FFT, c32, out of place"
         self.algo_name = "fft"

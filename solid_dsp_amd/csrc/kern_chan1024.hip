@@ -614,8 +614,8 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 // fft1024_pass_kernel<INV, TW, TPB> (bit-identical).  PRE: next-group loads issued before
 // the FFT (the rest after it).
 // LA / SA: the loads' / stores' cache policy (0 default, 2 nontemporal; lab variants), LA & 8
-// the skeleton without the FFT, LA / SA & 16 16-byte lanes on the strided side, LA & 32
-// XCD-ordered groups (lab)
+// the skeleton without the FFT (lab), LA / SA & 16 16-byte lanes on the strided side (LA & 16 in
+// the product), LA & 32 XCD-ordered groups (lab: 953 -> 970 us on the column pass)
 template <bool INV, bool TW, bool CFAST, bool OFAST, int TPB = 16, int PRE = 8, int LA = 0, int SA = 0>
 __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* __restrict__ y,
                                                   const cf* __restrict__ tw, const cf* __restrict__ twx,
@@ -649,8 +649,12 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
     const unsigned in_k = (unsigned)(cfast ? 64 * Si : S1) * 8u;
     const unsigned out_lane = (unsigned)(ofast ? ((t & (TPB - 1)) + (long long)(t >> kLog) * So) : (long long)t * So) * 8u;
     const unsigned out_k = (unsigned)(ofast ? 64 * So : T1) * 8u;
-    // LA / SA & 16 (lab only): 16-byte lanes on the strided side, lane t holding columns
-    // 2 (t & 7) and 2 (t & 7) + 1 of rows (t >> 3) + 128 m, m = k / 2 (the stride probe's lane shape)
+    // LA & 16 (the product when the input allows it): the strided-side loads in 16-byte lanes, lane t
+    // holding columns 2 (t & 7) and 2 (t & 7) + 1 of rows (t >> 3) + 128 m, m = k / 2: half the load
+    // instructions for the same bytes, the column pass 953 -> 918 us on cfg8, bit-identical
+    // (profiles/r05/lab/r05u_fftlab_lanes.log; tools/stride_probe.hip: 128-byte runs 3.4 % faster in
+    // 16-byte than in 8-byte lanes).  SA & 16 (lab only): the same for the strided-side stores
+    // (slower: 1042 us, the twiddle base per column pair costs more than the stores save)
     constexpr bool wide_in = (LA & 16) != 0 && cfast, wide_out = (SA & 16) != 0 && ofast;
     const unsigned in_lane16 = (unsigned)(2 * (t & 7) + (long long)(t >> 3) * Si) * 8u, in_k16 = (unsigned)(128 * Si) * 8u;
     const unsigned out_lane16 = (unsigned)(2 * (t & 7) + (long long)(t >> 3) * So) * 8u, out_k16 = (unsigned)(128 * So) * 8u;
@@ -850,9 +854,20 @@ bool try_launch_fft1024_pass_t(const FftPass& p, hipStream_t s, hipError_t* err)
         const long long groups = p.count / 16;
         const dim3 g2((unsigned)(groups < cus ? groups : cus));
         const bool cf_ = p.S1 == 1, of_ = p.T1 == 1;
-#define SDSP_PIPE4(INV, TW, C, O)                                                                                 \
-    hipLaunchKernelGGL((fft1024_pipe_kernel<INV, TW, C, O, LA, SA>), g2, dim3(1024), 0, s, (const cf*)p.x, (cf*)p.y, \
+        // 16-byte strided-side loads: every group's base and row offset 16-byte aligned
+        const bool wide = cf_ && ((uintptr_t)p.x & 15) == 0 && (p.S0 & 1) == 0 && (p.Si & 1) == 0;
+#define SDSP_PIPE5(INV, TW, C, O, LAV)                                                                              \
+    hipLaunchKernelGGL((fft1024_pipe_kernel<INV, TW, C, O, LAV, SA>), g2, dim3(1024), 0, s, (const cf*)p.x, (cf*)p.y, \
                        (const cf*)p.tw, (const cf*)p.twx, p.count, p.G, p.S0, p.S1, p.Si, p.T1, p.So)
+#define SDSP_PIPE4(INV, TW, C, O)                                            \
+    do {                                                                      \
+        if constexpr (C) {                                                    \
+            if (wide) SDSP_PIPE5(INV, TW, C, O, (LA | 16));                   \
+            else SDSP_PIPE5(INV, TW, C, O, LA);                               \
+        } else {                                                              \
+            SDSP_PIPE5(INV, TW, C, O, LA);                                    \
+        }                                                                     \
+    } while (0)
 #define SDSP_PIPE(INV, TW)                                                                         \
     do {                                                                                           \
         if (cf_) { if (of_) SDSP_PIPE4(INV, TW, true, true); else SDSP_PIPE4(INV, TW, true, false); }   \
@@ -865,6 +880,7 @@ bool try_launch_fft1024_pass_t(const FftPass& p, hipStream_t s, hipError_t* err)
         }
 #undef SDSP_PIPE
 #undef SDSP_PIPE4
+#undef SDSP_PIPE5
         *err = hipGetLastError();
         return true;
     }

@@ -65,6 +65,33 @@ def test_fft_large_and_any_size(n, method, prec):
         assert rel_rms(t.cpu().numpy(), y) <= (1e-6 if prec == np.complex64 else 1e-14)
 
 
+@pytest.mark.parametrize("d", [FFTDirection.FORWARD, FFTDirection.REVERSE])
+def test_fft_2p20_column_pass_lane_forms_agree(d):
+    """The 2^20-point column pass loads its strided side in 16-byte lanes when the input is
+    16-byte aligned and in 8-byte lanes otherwise (kern_chan1024.hip, fft1024_pipe_body
+    LA & 16): the same arithmetic, so the two must agree bit for bit, and with numpy."""
+    import torch
+    n, batch = 1 << 20, 2
+    rng = np.random.default_rng(7)
+    x = (rng.standard_normal((batch, n)) + 1j * rng.standard_normal((batch, n))).astype(np.complex64)
+    f = FFT(n, d, precision=np.complex64)
+    st = torch.cuda.current_stream()
+    a = torch.from_numpy(x.reshape(-1)).to("cuda")
+    ya = torch.empty_like(a)
+    f.execute_device(a, ya, batch, st)
+    b = torch.empty(batch * n + 1, dtype=torch.complex64, device="cuda")[1:]  # 8 bytes past alignment
+    assert b.data_ptr() % 16 == 8
+    b.copy_(a)
+    yb = torch.empty_like(a)
+    f.execute_device(b, yb, batch, st)
+    torch.cuda.synchronize()
+    ya, yb = ya.cpu().numpy(), yb.cpu().numpy()
+    assert bits_equal(ya, yb)
+    xs = x.astype(np.complex128)
+    ref = np.fft.fft(xs, axis=-1) if d == FFTDirection.FORWARD else np.fft.ifft(xs, axis=-1) * n
+    assert rel_rms(ya.reshape(batch, n), ref) <= 5e-6
+
+
 def test_fft_errors():
     with pytest.raises(sd.SdspError):
         FFT(0)

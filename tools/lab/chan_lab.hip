@@ -15,7 +15,8 @@ static int g_chan_lab = 0;
 static int g_fft_policy = 0;  // 4-step L = 1024 passes: bit 0 nontemporal loads, bit 1 nontemporal stores,
                               // bit 2 no inter-pass twiddle (ablation), 8 the pass skeleton
                               // (loads, staging, twiddle, stores; no FFT), 16 / 32 16-byte
-                              // lanes on the strided side of the loads / stores, 64 XCD-ordered
+                              // lanes on the strided side of the loads / stores (16: the
+                              // product since r05u, so the same as 0), 64 XCD-ordered
                               // groups
 
 bool try_launch_fft1024_pass(const FftPass& p_, hipStream_t s, hipError_t* err) {
