@@ -103,8 +103,9 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 
 }  // namespace
 
-// ABL selects compile-time variants of the segment transform.  The product kernel
-// is ABL = 0; tools/lab/ols_lab.hip instantiates the others for in-process A/B runs
+// ABL selects compile-time variants of the segment transform.  The product kernels
+// are ABL = 24 (one halo row, L <= 257) and ABL = 0 (longer filters), see launch_fir_ols_os;
+// tools/lab/ols_lab.hip instantiates the others for in-process A/B runs
 // (never part of libsdsp.so).  Bits: 1 block barriers at the wave-local phase
 // boundaries; 2 no HBM traffic (ablation: outputs dropped); 4 HBM traffic only
 // (ablation: no transform); 128 plain (not nontemporal) stores; 256 input rows
@@ -115,6 +116,9 @@ __device__ __forceinline__ f2 tw_pair(const f2 (&c)[3], const f2 (&d)[3], int k)
 // twiddle-base tables requested after the rows; 16777216 the rows issued exactly in the loop's
 // order (a scheduling barrier after each load); 33554432 the boundary segments as extra
 // workgroups of the interior launch (a branch at the kernel's entry);
+// 16 one halo row compiled in (h2 = 1: rows 1..15 stored without a test per row);
+// 8 the rows a neighbouring segment also reads when h2 = 1 (row 0, the halo, and row 15, the next
+// segment's halo) with temporal loads, the others nontemporal;
 // ablations of the per-segment table reads from L2: 2048 no spectrum loads, 4096 no
 // twiddle-base loads (wrong results, timing only); 8192 write-through (sc1) stores; 16384
 // plain (not nontemporal) input loads; 32768 all six twiddle bases loaded (the round-3 form;
@@ -128,6 +132,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
                                                long long n, int Lm1, int h2, f2* img, int t) {
     const int hi4 = t >> 4, lo4 = t & 15;
+    if constexpr ((ABL & 16) != 0) h2 = 1;  // one halo row compiled in (the launcher checks h2 == 1)
     // the segment's window x[base, base + 4096) as a raw buffer.  EDGE (the boundary segments of a
     // call, launched apart so that the interior kernel carries no boundary code: its presence
     // alone cost the interior segments 1.9 %, profiles/r05/lab/r05e_olsburst.log): past the end of
@@ -207,6 +212,8 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
                 const int r = (ABL & 256) ? 15 - i : (ABL & 2097152) ? 4 * (i & 3) + (i >> 2) : i;
                 if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
                 else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
+                else if ((ABL & 8) && (r == 0 || r == 15))
+                    v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
                 else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, kLdAux));
                 if constexpr ((ABL & 16777216) != 0) __builtin_amdgcn_sched_barrier(0);  // lab: issue in this order
             }
@@ -440,10 +447,17 @@ hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, const void* hist
     return hipGetLastError();
 }
 
+// the interior kernel's product variants: kOlsOneHalo | kOlsHaloTemporal when the halo is one
+// row (L <= 257, every cfg2-like filter), ABL = 0 for longer filters, 524288 the 16-byte-lane form
+// (SDSP_TUNE_OLS_KERNEL = 3)
+constexpr int kOlsHaloTemporal = 8, kOlsOneHalo = 16;
+
 hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
                              int Lm1, size_t channels, hipStream_t s, bool wide) {
-    return wide ? launch_fir_ols_os_t<524288>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0)
-                : launch_fir_ols_os_t<0>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0);
+    if (wide) return launch_fir_ols_os_t<524288>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0);
+    if (p.halo_rows == 1)
+        return launch_fir_ols_os_t<kOlsOneHalo | kOlsHaloTemporal>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0);
+    return launch_fir_ols_os_t<0>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0);
 }
 
 }  // namespace sdsp
