@@ -37,6 +37,11 @@ class Channelizer:
             L.lib().sdsp_chan_destroy(h)
             self._h = None
 
+    def set_tuning(self, key: int, value: int):
+        """Kernel-variant knobs (L.TUNE_CHAN_STREAMING, L.TUNE_CHAN_FRAMES_PER_BLOCK, L.TUNE_CHAN_XCD_ORDER;
+        performance only, same results)."""
+        L.check(L.lib().sdsp_chan_set_tuning(self._h, int(key), int(value)))
+
     def set_streams(self, streams: int):
         L.check(L.lib().sdsp_chan_set_streams(self._h, streams))
         self.streams = streams

@@ -221,9 +221,10 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // nontemporal stores (the round-3 product; the product's interior stores are write-through), 256
 // the scalar correction (the round-3 arithmetic; real f32), 512 every scan level (the round-4 scan),
 // 1024 compiled for one rate without exact carries, 2048 the lane shifts by one as DPP wave_shr
-// moves (real f32, D = 8)
+// moves (real f32, D = 8), 4096 the carry as the lane scan's element -1 (no separate fold), 8192
+// compiled for 4 workgroups per CU (<= 128 VGPRs)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
-__global__ void __launch_bounds__(kWsThreads)
+__global__ void __launch_bounds__(kWsThreads, (LAB & 8192) ? 4 : 1)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
                  const I* __restrict__ st_in, I* __restrict__ st_out, long long nd, int wc, int tpw, bool vec_ok,
@@ -367,8 +368,13 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 else s[d] = st_in[d];
             }
         }
-        // 3. fold the carry into lane 0, then the inclusive scan over lanes
-        if (!(lab & 2)) {
+        // 3. fold the carry into lane 0, then the inclusive scan over lanes.  carry_lane (LAB 4096,
+        //    warm-up scans only): the carry is the scan's element -1 instead -- at level k lane
+        //    2^k - 1 takes it as its predecessor (element -1 is never updated), so no separate fold;
+        //    its window [l - 2^nlev + 1, l] holds element -1 for l <= 2^nlev - 2, which covers the
+        //    lanes l <= wc - 2 whose carry term A^(B (l + 1)) carry is above the warm-up tolerance
+        const bool carry_lane = (LAB & 4096) != 0 && wc > 0;
+        if (!(lab & 2) && !carry_lane) {
             I a[D];
             sys_matvec<ND>(sP, carry, a);
             if (lane == 0) {
@@ -376,9 +382,10 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 for (int d = 0; d < D; ++d) s[d] = add_(s[d], a[d]);
             }
         }
+        const int nlev_t = carry_lane && nlev < 1 ? 1 : nlev;
 #pragma unroll
         for (int k = 0; k < 6 && !(lab & 2); ++k) {
-            if (k >= nlev) break;  // the terms of lanes >= 2^nlev back have decayed (see nlev)
+            if (k >= nlev_t) break;  // the terms of lanes >= 2^nlev back have decayed (see nlev)
             const int off = 1 << k;
             I prev[D], a[D];
             if (k == 0) {
@@ -387,8 +394,14 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
 #pragma unroll
                 for (int d = 0; d < D; ++d) prev[d] = shfl_up_v(s[d], off);
             }
+            if constexpr ((LAB & 4096) != 0) {
+                if (carry_lane) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) prev[d] = lane == off - 1 ? carry[d] : prev[d];
+                }
+            }
             sys_matvec<ND>(sP + k * D * D, prev, a);
-            if (lane >= off) {
+            if (lane >= off - (carry_lane ? 1 : 0)) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) s[d] = add_(s[d], a[d]);
             }
@@ -917,9 +930,13 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
 }
 
 template <int CB> int wscan_tpw(long long nch) {
-    // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible
+    // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible.
+    // 128-byte chunks stop at 5 tiles: cfg3 (2^30 real f32, 20 back-to-back calls, 16 interleaved
+    // rounds) ran 1.653 / 1.650 / 1.627 / 1.615 / 1.640 ms at 8 / 7 / 6 / 5 / 4 tiles, outputs within
+    // 1.1e-8 rel-RMS of each other (the warm-up boundaries move; profiles/r05/lab/r05ze_iirburst.log)
+    constexpr int kMax = CB == 128 ? 5 : 8;
     int tpw = (int)(nch / (64LL * 4096));
-    return tpw < 1 ? 1 : (tpw > 8 ? 8 : tpw);
+    return tpw < 1 ? 1 : (tpw > kMax ? kMax : tpw);
 }
 
 // LAB: sos_wscan_kernel (0 = the product kernel); tpw_force > 0 sets the tiles per wave of a

@@ -23,7 +23,7 @@ for s in ${STEPS:-pytest}; do
         olsburst) OLS_BURST=${BURST:-20} OLS_ROUNDS=${BROUNDS:-6} OLS_CASES=${OLS_CASES:-0,256,4,260} run olsburst 600 python -u tools/ols_lab.py ;;
         iirab) IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirab 600 python -u tools/iir_ab.py ;;
         # iirpmc: one PMC pass (SQ instruction counts) over the lab ablations in IIR_CASES
-        iirpmc) IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:1,0:2,0:4,0:7} run iirpmc 300 rocprofv3 --pmc ${PMC:-SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES} \
+        iirpmc) IIR_LAB=1 IIR_CASES=${IIR_CASES:-2,2:1,2:2,2:4,2:7} run iirpmc 300 rocprofv3 --pmc ${PMC:-SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES} \
                 --output-format csv -d gpurun_out/${TAG}_iirpmc -o run -- python -u tools/iir_ab.py ;;
         iirburst) IIR_BURST=${BURST:-20} IIR_LAB=1 IIR_CASES=${IIR_CASES:-0,0:4} run iirburst 600 python -u tools/iir_ab.py ;;
         chanab) run chanab 600 python -u tools/chan_ab.py ;;

@@ -10,7 +10,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def main(rounds=8, log2n=30):
+def main(rounds=int(os.environ.get("IIR_ROUNDS", "8")), log2n=30):
     import torch
     lab = bool(os.environ.get("IIR_LAB"))  # cases "variant:ablation" on the lab build (tools/lab.mk)
     if lab or os.environ.get("IIR_LIB"):  # IIR_LIB: e.g. an older build, same box

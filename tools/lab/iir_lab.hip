@@ -42,6 +42,11 @@ static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw)
         // codes past the LAB bits (the value's low 12 bits): 3072 = the FORM 2 kernel (no register
         // prefetch) with the DPP lane shifts (LAB 2048: 116 VGPRs, 4 waves per SIMD)
         case 3072: return launch_wscan_t<float, float, 4, CB, 2, 0, 2048>(a, st, tpw);
+        // 3073: LAB 4096 (the carry as the scan's element -1); 3074: LAB 4096 + 1024
+        case 3073: return lab_cfg3<CB, 4096>(a, st, tpw);
+        case 3074: return lab_cfg3<CB, 5120>(a, st, tpw);
+        // 3075: LAB 4096 + 8192 (4 workgroups per CU)
+        case 3075: return lab_cfg3<CB, 12288>(a, st, tpw);
         default: return lab_cfg3<CB, 0>(a, st, tpw);
     }
 }
