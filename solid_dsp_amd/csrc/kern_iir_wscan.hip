@@ -931,10 +931,12 @@ hipError_t launch_wscan2_s(const IirArgs& a, hipStream_t st) {
 
 template <int CB> int wscan_tpw(long long nch) {
     // tiles per wave: long segments amortise the wc warm-up chunks; keep >= ~4k waves when possible.
-    // 128-byte chunks stop at 5 tiles: cfg3 (2^30 real f32, 20 back-to-back calls, 16 interleaved
+    // At most 5 tiles: cfg3 (2^30 real f32, 128-byte chunks, 20 back-to-back calls, 16 interleaved
     // rounds) ran 1.653 / 1.650 / 1.627 / 1.615 / 1.640 ms at 8 / 7 / 6 / 5 / 4 tiles, outputs within
-    // 1.1e-8 rel-RMS of each other (the warm-up boundaries move; profiles/r05/lab/r05ze_iirburst.log)
-    constexpr int kMax = CB == 128 ? 5 : 8;
+    // 1.1e-8 rel-RMS of each other (the warm-up boundaries move; profiles/r05/lab/r05ze_iirburst.log);
+    // cfg12 (256-byte chunks) 1.670 -> 1.643 ms at 5 instead of 8 (alternating bench lines,
+    // profiles/r05/lab/r05zh_libab_cfg12.log)
+    constexpr int kMax = 5;
     int tpw = (int)(nch / (64LL * 4096));
     return tpw < 1 ? 1 : (tpw > kMax ? kMax : tpw);
 }
