@@ -980,7 +980,7 @@ class Cfg11ActiveLag:
         self.samples_per_step = total
         self.bytes_per_step = 32 * total
         self.dtype = "c64 (f64 coefficients, Complex<f64> samples, reference summation order)"
-        self.kernel = "sos_serial_lds_kernel<1, double, c64> (one lane per channel, 256-byte runs staged through LDS)"
+        self.kernel = "sos_serial_lds_kernel<1, double, c64> (one lane per channel, 1 KB runs per channel staged through LDS)"
         self.parity_check = "bit mismatches vs the f64 restatement over 16 channels (must be 0)"
         self.workload = "cfg11: active_lag IIRFilter<f64, Complex<f64>> bank, 2^16 channels x 2^12 samples"
         self.algo_name = "iir_serial_bank"

@@ -100,10 +100,18 @@ sos_serial_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restric
 }
 
 // ---------------------------------------------------------------- serial SOS, LDS-staged
+// bytes per channel and tile: 1 KB runs per channel (cfg11: 1.72 -> 1.47 ms against 256-byte runs,
+// 512-byte runs 1.74 ms; alternating whole bench lines, profiles/r05/lab/r05zk_libab_cfg11.log).  The
+// 64 KB tile leaves room for two workgroups per CU and the prefetched tile holds 256 VGPRs per lane;
+// the longer runs, not the occupancy, are what the HBM stream rewards (a -D override builds the
+// A/B libraries)
+#ifndef SDSP_SERIAL_LDS_RUN
+#define SDSP_SERIAL_LDS_RUN 1024
+#endif
 // The same recurrence (lane = channel, reference order, bit-identical) for banks of
 // >= 64 channels without rate change: a one-wave workgroup serves 64 channels and
-// moves them through LDS in tiles of 256 bytes per channel, so HBM sees coalesced
-// 256-byte runs instead of one element per lane 8n bytes apart (measured 2.4x the
+// moves them through LDS in tiles of SDSP_SERIAL_LDS_RUN bytes per channel, so HBM sees coalesced
+// runs instead of one element per lane 8n bytes apart (measured 2.4x the
 // algorithmic traffic on the active_lag bank), with the next tile's loads in flight
 // while the current one runs.
 template <int S, typename C, typename I>
@@ -111,7 +119,10 @@ __global__ void __launch_bounds__(64)
 sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                       const I* __restrict__ st_in, I* __restrict__ st_out, long long n, int channels, bool vec_ok) {
     using v4u = unsigned __attribute__((ext_vector_type(4)));
-    constexpr int kRun = 256, E = 16 / (int)sizeof(I), T = kRun / (int)sizeof(I), kRow = kRun + 16;
+    constexpr int kRun = SDSP_SERIAL_LDS_RUN, E = 16 / (int)sizeof(I), T = kRun / (int)sizeof(I), kRow = kRun + 16;
+    constexpr int NV = kRun / 16;  // 16-byte vectors per channel and tile
+    constexpr int kLogNV = __builtin_ctz(NV);
+    static_assert((NV & (NV - 1)) == 0, "power-of-two tiles");
     __shared__ __attribute__((aligned(16))) char lds[64 * kRow];
     const int lane = threadIdx.x;
     const long long c0 = (long long)blockIdx.x * 64;
@@ -123,30 +134,26 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
         w1[s] = lane < nch ? st_in[(long long)ch * 2 * S + 2 * s] : zero_v<I>();
         w2[s] = lane < nch ? st_in[(long long)ch * 2 * S + 2 * s + 1] : zero_v<I>();
     }
-    // vector v of a tile: channel v >> 4, 16-byte part v & 15
-    auto vaddr = [&](long long k0, int v) -> long long { return (c0 + (v >> 4)) * n + k0 + (long long)(v & 15) * E; };
-    v4u pre[16];
-    auto load_tile = [&](long long k0) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int v = lane + 64 * j;
-            pre[j] = (v >> 4) < nch ? *reinterpret_cast<const v4u*>(x + vaddr(k0, v)) : v4u{0, 0, 0, 0};
-        }
-    };
-    const bool fast = vec_ok;
+    // vector v of a tile: channel v >> kLogNV, 16-byte part v & (NV - 1)
+    auto vaddr = [&](long long k0, int v) -> long long { return (c0 + (v >> kLogNV)) * n + k0 + (long long)(v & (NV - 1)) * E; };
+    v4u pre[NV];
+    // the pipelined path takes whole workgroups only: its per-vector offsets are a lane offset plus a
+    // scalar offset, and rows past the last channel are not left to the descriptor's range check
+    // (the partial last workgroup of a bank runs the element-wise loop below)
+    const bool fast = vec_ok && nch == 64;
     long long kstart = 0;
     if (fast && (unsigned long long)n * 64ull * sizeof(I) < (1ull << 32)) {
         // whole tiles, pipelined without branches around memory operations: buffer loads and stores
-        // bounded by the workgroup's channels (rows past nch read zeros and drop their stores), the
+        // through a descriptor that is empty past the last whole tile (no traffic), the
         // loop rotated so each tile is staged in the iteration that loaded it -- the compiler's wait
         // for the loads then sits behind only that iteration's stores
         const long long nfull = n / T * T;
-        unsigned off[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int v = lane + 64 * j;
-            off[j] = (unsigned)(((long long)(v >> 4) * n + (long long)(v & 15) * E) * (long long)sizeof(I));
-        }
+        // vector v = lane + 64 j sits at channel (lane >> kLogNV) + j (64 / NV), part lane & (NV - 1):
+        // one per-lane offset plus a wave-uniform j (64 / NV) n sizeof(I) (the instruction's scalar
+        // offset), so the tile's NV offsets hold no registers
+        const unsigned off0 = (unsigned)(((long long)(lane >> kLogNV) * n + (long long)(lane & (NV - 1)) * E) *
+                                         (long long)sizeof(I));
+        const int jstride = (int)((64 / NV) * n * (long long)sizeof(I));
         auto rsrc = [&](const void* base, long long k0) {
             const bool ok = k0 < nfull;
             const unsigned nrec = ok ? (unsigned)(((long long)nch * n - k0) * (long long)sizeof(I)) : 0u;
@@ -156,13 +163,16 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
         auto ld = [&](long long k0) {
             const auto r = rsrc(x, k0);
 #pragma unroll
-            for (int j = 0; j < 16; ++j) pre[j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off[j], 0, 0));
+            for (int j = 0, so = 0; j < NV; ++j, so += jstride) {
+                asm volatile("" : "+s"(so));  // formed here: not NV values hoisted into (spilled) SGPRs
+                pre[j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off0, so, 0));
+            }
         };
         auto stage = [&] {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
+            for (int j = 0; j < NV; ++j) {
                 const int v = lane + 64 * j;
-                *reinterpret_cast<v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16) = pre[j];
+                *reinterpret_cast<v4u*>(lds + (v >> kLogNV) * kRow + (v & (NV - 1)) * 16) = pre[j];
             }
         };
         if (nfull > 0) {
@@ -178,10 +188,11 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
                 __builtin_amdgcn_wave_barrier();
                 const auto r = rsrc(y, k0);
 #pragma unroll
-                for (int j = 0; j < 16; ++j) {
+                for (int j = 0, so = 0; j < NV; ++j, so += jstride) {
                     const int v = lane + 64 * j;
+                    asm volatile("" : "+s"(so));
                     __builtin_amdgcn_raw_buffer_store_b128(
-                        *reinterpret_cast<const v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16), r, off[j], 0, 0);
+                        *reinterpret_cast<const v4u*>(lds + (v >> kLogNV) * kRow + (v & (NV - 1)) * 16), r, off0, so, 0);
                 }
                 __builtin_amdgcn_s_waitcnt(0xC07F);
                 __builtin_amdgcn_wave_barrier();
@@ -190,16 +201,17 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
         }
         kstart = nfull;  // the ragged tail (if any) below
     }
-    if (fast && kstart == 0 && n >= T) load_tile(0);
+    // the ragged tail, a partial workgroup, or calls past 32-bit buffer offsets: whole tiles copied
+    // through LDS without a prefetch, partial ones element by element
     for (long long k0 = kstart; k0 < n; k0 += T) {
         const bool full = fast && k0 + T <= n;
         if (full) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
+#pragma unroll 4
+            for (int j = 0; j < NV; ++j) {
                 const int v = lane + 64 * j;
-                *reinterpret_cast<v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16) = pre[j];
+                *reinterpret_cast<v4u*>(lds + (v >> kLogNV) * kRow + (v & (NV - 1)) * 16) =
+                    *reinterpret_cast<const v4u*>(x + vaddr(k0, v));
             }
-            if (k0 + 2 * T <= n) load_tile(k0 + T);  // next tile in flight during this one
         } else {
             for (int i = lane; i < 64 * T; i += 64) {
                 const int cl = i / T, e = i % T;
@@ -215,12 +227,11 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_wave_barrier();
         if (full) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
+#pragma unroll 4
+            for (int j = 0; j < NV; ++j) {
                 const int v = lane + 64 * j;
-                if ((v >> 4) < nch)
-                    *reinterpret_cast<v4u*>(y + vaddr(k0, v)) =  // plain: nontemporal +1.7 % (cfg11)
-                        *reinterpret_cast<const v4u*>(lds + (v >> 4) * kRow + (v & 15) * 16);
+                *reinterpret_cast<v4u*>(y + vaddr(k0, v)) =  // plain: nontemporal +1.7 % (cfg11)
+                    *reinterpret_cast<const v4u*>(lds + (v >> kLogNV) * kRow + (v & (NV - 1)) * 16);
             }
         } else {
             for (int i = lane; i < 64 * T; i += 64) {
