@@ -528,13 +528,13 @@ __global__ void __launch_bounds__(64) agc_pipe_kernel(const AgcSample<CPLX>* __r
         gthr = pow(10.0, -s.squelch_threshold / 20.0);
     }
     const long long nfull = n / S * S;
-    // lane e = t + 64 k of a row group: channel e / S = t / S + k (64 / S), sample e % S = t % S of the
-    // chunk, so its offset is a lane part plus a wave-uniform k (64 / S) n SZ (the instruction's scalar
-    // offset: no register per k).  Whole workgroups only (the launcher runs a bank's last channels
-    // past a multiple of 64 on agc_kernel), so no row lies past the last channel.
-    static_assert(64 % S == 0, "chunk divides the wave");
-    const unsigned off0 = (unsigned)(((long long)(t / S) * n + t % S) * SZ);
-    const int kstride = (int)((64 / S) * n * SZ);
+    // lane e = t + 64 k of a row group: channel e / S, sample e % S of the chunk
+    unsigned off[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        const int e = t + 64 * k;
+        off[k] = (unsigned)(((long long)(e / S) * n + e % S) * SZ);
+    }
     V r[S];
     // chunk at i0 (whole chunks only; past nfull: an empty descriptor, no traffic)
     auto rsrc = [&](const void* base, long long i0) {
@@ -546,10 +546,9 @@ __global__ void __launch_bounds__(64) agc_pipe_kernel(const AgcSample<CPLX>* __r
     auto load_chunk = [&](long long i0) {
         const auto rx = rsrc(x, i0);
 #pragma unroll
-        for (int k = 0, so = 0; k < S; ++k, so += kstride) {
-            asm volatile("" : "+s"(so));  // formed here: not S values hoisted into (spilled) SGPRs
-            if constexpr (CPLX) r[k] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rx, off0, so, 0));
-            else r[k] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rx, off0, so, 0));
+        for (int k = 0; k < S; ++k) {
+            if constexpr (CPLX) r[k] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rx, off[k], 0, 0));
+            else r[k] = __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b64(rx, off[k], 0, 0));
         }
     };
     auto stage = [&] {  // the loaded chunk into the LDS rows
@@ -574,12 +573,11 @@ __global__ void __launch_bounds__(64) agc_pipe_kernel(const AgcSample<CPLX>* __r
         __syncthreads();
         const auto ry = rsrc(y, i0);
 #pragma unroll
-        for (int k = 0, so = 0; k < S; ++k, so += kstride) {
+        for (int k = 0; k < S; ++k) {
             const int e = t + 64 * k;
-            asm volatile("" : "+s"(so));
             const V v = __builtin_bit_cast(V, buf[(e / S) * (S + 1) + e % S]);
-            if constexpr (CPLX) __builtin_amdgcn_raw_buffer_store_b128(v, ry, off0, so, 0);
-            else __builtin_amdgcn_raw_buffer_store_b64(v, ry, off0, so, 0);
+            if constexpr (CPLX) __builtin_amdgcn_raw_buffer_store_b128(v, ry, off[k], 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b64(v, ry, off[k], 0, 0);
         }
         __syncthreads();
         stage();
@@ -768,24 +766,14 @@ hipError_t launch_agc(bool cplx, const void* x, void* y, size_t n, void* state, 
                       bool pipe) {
     if (n == 0 || channels == 0) return hipSuccess;
     dim3 grid((unsigned)((channels + 63) / 64));
-    const size_t whole = channels / 64 * 64;  // the pipelined kernel takes whole workgroups of channels
-    if (pipe && (long long)n < kAgcPipeMaxN && whole > 0) {
-        const dim3 g1((unsigned)(whole / 64));
+    if (pipe && (long long)n < kAgcPipeMaxN) {
         if (cplx)
-            hipLaunchKernelGGL((agc_pipe_kernel<true, kAgcPipeS>), g1, dim3(64), 0, s, (const AgcSample<true>*)x,
-                               (AgcSample<true>*)y, (long long)n, (sdsp_agc_state*)state, (long long)whole);
+            hipLaunchKernelGGL((agc_pipe_kernel<true, kAgcPipeS>), grid, dim3(64), 0, s, (const AgcSample<true>*)x,
+                               (AgcSample<true>*)y, (long long)n, (sdsp_agc_state*)state, (long long)channels);
         else
-            hipLaunchKernelGGL((agc_pipe_kernel<false, kAgcPipeS>), g1, dim3(64), 0, s, (const AgcSample<false>*)x,
-                               (AgcSample<false>*)y, (long long)n, (sdsp_agc_state*)state, (long long)whole);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess || whole == channels) return e;
-        // the last channels past a multiple of 64 (independent recurrences: exact in either kernel)
-        const size_t rest = channels - whole, sz = cplx ? sizeof(AgcSample<true>) : sizeof(AgcSample<false>);
-        x = (const char*)x + whole * n * sz;
-        y = (char*)y + whole * n * sz;
-        state = (sdsp_agc_state*)state + whole;
-        channels = rest;
-        grid = dim3(1);
+            hipLaunchKernelGGL((agc_pipe_kernel<false, kAgcPipeS>), grid, dim3(64), 0, s, (const AgcSample<false>*)x,
+                               (AgcSample<false>*)y, (long long)n, (sdsp_agc_state*)state, (long long)channels);
+        return hipGetLastError();
     }
     if (cplx)
         hipLaunchKernelGGL(agc_kernel<true>, grid, dim3(64), 0, s, (const AgcSample<true>*)x, (AgcSample<true>*)y,
