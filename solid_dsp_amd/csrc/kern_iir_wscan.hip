@@ -222,7 +222,7 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // the scalar correction (the round-3 arithmetic; real f32), 512 every scan level (the round-4 scan),
 // 1024 compiled for one rate without exact carries, 2048 the lane shifts by one as DPP wave_shr
 // moves (real f32, D = 8), 4096 the carry as the lane scan's element -1 (no separate fold), 8192
-// compiled for 4 workgroups per CU (<= 128 VGPRs)
+// compiled for 4 workgroups per CU (<= 128 VGPRs), 16384 blocks in launch order (not XCD-ordered)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__(kWsThreads, (LAB & 8192) ? 4 : 1)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -270,7 +270,8 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     // XCD-ordered blocks (gridDim.x is a multiple of 8): block b runs on XCD b % 8 and
     // takes the (b / 8)-th block of that XCD's contiguous eighth, so each XCD streams
     // one window of neighbouring segments (cfg3: -1.6 %, the HBM-only pattern -2 %)
-    const long long bx = (long long)(blockIdx.x & 7) * (gridDim.x / 8) + (blockIdx.x >> 3);
+    const long long bx = (LAB & 16384) ? (long long)blockIdx.x  // lab: launch order
+                                       : (long long)(blockIdx.x & 7) * (gridDim.x / 8) + (blockIdx.x >> 3);
     const long long gw = bx * kWsWaves + wave;        // wave's segment
     const long long segc = (long long)tpw * 64 - wc;  // chunks per segment
     const long long c_lo = gw * segc;                 // first chunk of the segment
