@@ -145,7 +145,9 @@ typedef enum {
                                      0 = per-frame kernel */
     SDSP_TUNE_CHAN_FRAMES_PER_BLOCK = 9, /* streaming channeliser: frames per workgroup (0 = automatic, 64..256) */
     SDSP_TUNE_OLS_KERNEL = 14,   /* overlap-save segments (16-byte aligned rows): 0 (default) one-shot
-                                    XCD-ordered kernel for every segment (it also writes the next history),
+                                    XCD-ordered kernels: the interior segments in one launch (one halo row
+                                    compiled in when L <= 257), the boundary segments and the next history
+                                    in a second,
                                     1 persistent packed kernel for the interior segments (L <= 1025),
                                     2 scalar kernel, 3 the one-shot kernel with 16-byte lanes */
     SDSP_TUNE_CHAN_XCD_ORDER = 15, /* streaming channeliser: 1 (default) = each XCD walks a contiguous
