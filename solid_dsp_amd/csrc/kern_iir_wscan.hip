@@ -222,9 +222,10 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // the scalar correction (the round-3 arithmetic; real f32), 512 every scan level (the round-4 scan),
 // 1024 compiled for one rate without exact carries, 2048 the lane shifts by one as DPP wave_shr
 // moves (real f32, D = 8), 4096 the carry as the lane scan's element -1 (no separate fold), 8192
-// compiled for 4 workgroups per CU (<= 128 VGPRs), 16384 blocks in launch order (not XCD-ordered)
+// compiled for 4 workgroups per CU (<= 128 VGPRs), 16384 blocks in launch order (not XCD-ordered),
+// 32768 four-wave workgroups (the form before one-wave workgroups)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
-__global__ void __launch_bounds__(kWsThreads, (LAB & 8192) ? 4 : 1)
+__global__ void __launch_bounds__((LAB & 32768) ? kWsThreads : 64, (LAB & 8192) ? 4 : 1)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
                  const C* __restrict__ P /* [6][D][D] */, const C* __restrict__ Cr /* [B][D] */,
                  const I* __restrict__ st_in, I* __restrict__ st_out, long long nd, int wc, int tpw, bool vec_ok,
@@ -250,8 +251,12 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     char* slab = lds_raw + wave * kSlabBytes;
     char* row = slab + lane * kRowBytes;
-    C* sP = reinterpret_cast<C*>(lds_raw + kWsWaves * kSlabBytes);
-    for (int i = threadIdx.x; i < 6 * D * D; i += kWsThreads) sP[i] = P[i];
+    // one-wave workgroups: a wave's slab and registers return to the CU when its own segment ends
+    // (cfg3 1.565 -> 1.546 ms, bit-identical, profiles/r05/lab/r05zq_iirburst_onewave.log); LAB 32768:
+    // the four-wave workgroups of rounds 2-5 (lab)
+    constexpr int kWaves = (LAB & 32768) ? kWsWaves : 1;
+    C* sP = reinterpret_cast<C*>(lds_raw + kWaves * kSlabBytes);
+    for (int i = threadIdx.x; i < 6 * D * D; i += 64 * kWaves) sP[i] = P[i];
     __syncthreads();
 
     const int ch = blockIdx.y;
@@ -272,7 +277,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
     // one window of neighbouring segments (cfg3: -1.6 %, the HBM-only pattern -2 %)
     const long long bx = (LAB & 16384) ? (long long)blockIdx.x  // lab: launch order
                                        : (long long)(blockIdx.x & 7) * (gridDim.x / 8) + (blockIdx.x >> 3);
-    const long long gw = bx * kWsWaves + wave;        // wave's segment
+    const long long gw = bx * kWaves + wave;          // wave's segment
     const long long segc = (long long)tpw * 64 - wc;  // chunks per segment
     const long long c_lo = gw * segc;                 // first chunk of the segment
     const long long k_lo = c_lo * B;
@@ -957,22 +962,23 @@ hipError_t launch_wscan_t(const IirArgs& a, hipStream_t st, int tpw_force = 0) {
     const bool exact = a.wc == 0;  // exact inter-wave carries: aggregate pass + carry scan first
     if (exact && (!a.Phi || !a.G || !a.Cin || (size_t)waves > a.scratch_waves)) return hipErrorInvalidValue;
     // whole eighths for the XCD-ordered block map (surplus blocks find no segment and return)
-    dim3 grid((unsigned)((waves + 8 * kWsWaves - 1) / (8 * kWsWaves) * 8), (unsigned)a.channels);
+    constexpr int kWaves = (LAB & 32768) ? kWsWaves : 1;  // waves per workgroup (see sos_wscan_kernel)
+    dim3 grid((unsigned)((waves + 8 * kWaves - 1) / (8 * kWaves) * 8), (unsigned)a.channels);
     // 16-byte vector path: aligned bases and channel strides
     const bool vec_ok = reinterpret_cast<uintptr_t>(a.x) % 16 == 0 && reinterpret_cast<uintptr_t>(a.y) % 16 == 0 &&
                         (a.channels == 1 || (nd * (long long)sizeof(I)) % 16 == 0);
-    const size_t lds = (size_t)kWsWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * D * D);
+    const size_t lds = (size_t)kWaves * WsGeom<CB>::kSlabBytes + sizeof(C) * (6 * D * D);
     const long long j0 = a.Md > 1 ? (long long)((a.Md - 1 - a.phase) % a.Md) : 0;  // first emitting domain index
     const long long ny = a.Md > 1 ? (long long)a.nout : nd;
     if (exact) {
-        hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x,
+        hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(64 * kWaves), lds, st, (const I*)a.x,
                            (I*)a.y, (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out,
                            nd, 0, tpw, vec_ok, a.Mi, a.Md, j0, ny, (const I*)nullptr, (I*)a.G, waves);
         hipLaunchKernelGGL((wscan_carry_kernel<D, ND ? 0 : S, C, I>), dim3((unsigned)a.channels), dim3(256), 0, st,
                            (const I*)a.G, (I*)a.Cin, (const C*)a.Phi + (size_t)(tpw - 1) * D * D, (const I*)a.st_in,
                            waves, (const C*)a.coefs);
     }
-    hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(kWsThreads), lds, st, (const I*)a.x, (I*)a.y,
+    hipLaunchKernelGGL((sos_wscan_kernel<S, ND, C, I, CB, FORM, LAB>), grid, dim3(64 * kWaves), lds, st, (const I*)a.x, (I*)a.y,
                        (const C*)a.coefs, (const C*)a.P, (const C*)a.Cr, (const I*)a.st_in, (I*)a.st_out, nd, a.wc,
                        tpw, vec_ok, a.Mi, a.Md, j0, ny, exact ? (const I*)a.Cin : (const I*)nullptr, (I*)nullptr,
                        waves);

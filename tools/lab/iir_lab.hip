@@ -49,6 +49,8 @@ static hipError_t lab_cfg3_ab(const IirArgs& a, hipStream_t st, int ab, int tpw)
         case 3075: return lab_cfg3<CB, 12288>(a, st, tpw);
         // 3076: LAB 16384 (blocks in launch order)
         case 3076: return lab_cfg3<CB, 16384>(a, st, tpw);
+        // 3077: LAB 32768 (four-wave workgroups, the form before the one-wave product)
+        case 3077: return lab_cfg3<CB, 32768>(a, st, tpw);
         default: return lab_cfg3<CB, 0>(a, st, tpw);
     }
 }
