@@ -413,6 +413,7 @@ typedef struct sdsp_nco sdsp_nco;
 SDSP_API int sdsp_nco_create(sdsp_nco** out, int device);                     /* NCO::new  :36-50 */
 SDSP_API void sdsp_nco_destroy(sdsp_nco* h);
 SDSP_API int sdsp_nco_reset(sdsp_nco* h);                                     /* :53-56 */
+SDSP_API uint32_t sdsp_nco_constrain(double theta);                           /* constrain :175-187 */
 SDSP_API int sdsp_nco_set_frequency(sdsp_nco* h, double delta_theta);         /* :59-61 */
 SDSP_API int sdsp_nco_adjust_frequency(sdsp_nco* h, double dt);               /* :64-66 */
 SDSP_API double sdsp_nco_get_frequency(const sdsp_nco* h);                    /* :69-76 */
@@ -477,6 +478,7 @@ SDSP_API int sdsp_agc_set_signal_level(sdsp_agc* h, double level);              
 SDSP_API int sdsp_agc_set_rssi(sdsp_agc* h, double rssi);                       /* :458-466 */
 SDSP_API int sdsp_agc_set_gain(sdsp_agc* h, double gain);                       /* :497-504 */
 SDSP_API int sdsp_agc_set_scale(sdsp_agc* h, double scale);                     /* :535-542 */
+SDSP_API int sdsp_agc_update_squelch_mode(sdsp_agc* h);                        /* :631-677, each channel */
 SDSP_API int sdsp_agc_squelch_enable(sdsp_agc* h);                              /* :589-591 */
 SDSP_API int sdsp_agc_squelch_disable(sdsp_agc* h);                             /* :594-596 */
 SDSP_API int sdsp_agc_squelch_set_threshold(sdsp_agc* h, double threshold);     /* :612-614 */
@@ -498,6 +500,27 @@ SDSP_API int sdsp_bandwidth_copy_device(const void* d_src, void* d_dst, size_t b
 SDSP_API int sdsp_firdes_kaiser(size_t n, double fc, double as, double mu, double* h);
 SDSP_API int sdsp_firdes_notch(size_t m, double f0, double as, double* h);
 SDSP_API double sdsp_kaiser_beta(double as);
+/* The rest of solid::filter::firdes (src/filter/firdes/mod.rs:46-640), host f64 like the
+ * reference.  Status codes are FirdesErrorCode + 1: 1 Bandwidth, 2 StopBandLevel, 3 Mu,
+ * 4 SemiLength, 5 FilterSize, 6 FFTSize.  `method`: 0 EstimationMethod::Kaiser, 1 Herrmann. */
+/* estimate_required_filter_length :71-94 (the f64 estimate `as usize`, saturating) */
+SDSP_API int sdsp_firdes_estimate_length(double df, double as, int method, size_t* len);
+/* estimate_required_filter_length_kaiser :199-211 / _herrmann :213-240 */
+SDSP_API int sdsp_firdes_estimate_length_kaiser(double df, double as, double* len);
+SDSP_API int sdsp_firdes_estimate_length_herrmann(double df, double as, double* len);
+/* estimate_required_filter_stop_band_attenuation :117-145 (bisection, 20 steps) */
+SDSP_API int sdsp_firdes_estimate_stop_band_attenuation(double df, size_t n, int method, double* as);
+/* estimate_required_filter_transition :168-196 */
+SDSP_API int sdsp_firdes_estimate_transition(double as, size_t n, int method, double* df);
+/* firdes_doppler :389-419 (Bessel J0 of src/math/mod.rs:102-146, Kaiser window beta 4) */
+SDSP_API int sdsp_firdes_doppler(size_t n, double fd, double k, double theta, double* h);
+/* filter_autocorrelation :443-456, filter_crosscorrelation :487-527 */
+SDSP_API double sdsp_filter_autocorrelation(const double* h, size_t n, ptrdiff_t lag);
+SDSP_API double sdsp_filter_crosscorrelation(const double* h, size_t nh, const double* g, size_t ng, ptrdiff_t lag);
+/* filter_isi :552-577: (rms, max); (0, 0) when n != 2 sps delay + 1 */
+SDSP_API int sdsp_filter_isi(const double* h, size_t n, size_t sps, size_t delay, double* rms, double* max);
+/* filter_energy :602-640: relative out-of-band energy over fft_size bins (DotProduct FORWARD per bin) */
+SDSP_API int sdsp_filter_energy(const double* h, size_t n, double fc, size_t fft_size, double* energy);
 /* PLL loop filters (src/filter/iirdes/pll/mod.rs:24-99) */
 SDSP_API int sdsp_active_lag(double bw, double zeta, double k, double* num3, double* den3);
 SDSP_API int sdsp_active_proportional_integral(double bw, double zeta, double k, double* num3, double* den3);

@@ -12,6 +12,9 @@
 //   firdes_kaiser        src/filter/firdes/mod.rs:278-305
 //   firdes_notch         src/filter/firdes/mod.rs:329-368
 //   estimate_* lengths   src/filter/firdes/mod.rs:71-240
+//   besselj              src/math/mod.rs:102-146
+//   firdes_doppler       src/filter/firdes/mod.rs:389-419
+//   filter_autocorrelation / crosscorrelation / isi / energy   src/filter/firdes/mod.rs:443-640
 //   active_lag / active_proportional_integral   src/filter/iirdes/pll/mod.rs:24-99
 // ============================================================================
 #include <cmath>
@@ -78,6 +81,22 @@ double herrmann(double df, double as) {  // src/filter/firdes/mod.rs:213-240
     return (d_inf - f * df * df) / df + 1.0;
 }
 double kaiser_len(double df, double as) { return (as - 7.95) / (14.26 * df); }  // :199-211
+double besselj(double z, double nu) {  // src/math/mod.rs:102-146
+    if (z == 0.0) return nu == 0.0 ? 1.0 : 0.0;
+    if (z < 0.001 * std::sqrt(nu + 1.0)) return std::pow(0.5 * z, nu) / gamma_(nu + 1.0);
+    double J = 0.0;
+    double abs_nu = std::fabs(nu);
+    for (size_t i = 0; i < 128; ++i) {
+        double t0 = 2.0 * (double)i + abs_nu;
+        double t1 = t0 * std::log(z);
+        double t2 = t0 * std::log(2.0);
+        double t3 = lngamma((double)i + 1.0);
+        double t4 = lngamma(abs_nu + (double)i + 1.0);
+        if (i % 2 == 0) J += std::exp(t1 - t2 - t3 - t4);
+        else J -= std::exp(t1 - t2 - t3 - t4);
+    }
+    return J;
+}
 
 inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -158,6 +177,77 @@ double orc_estimate_req_filter_df(double as, size_t n, int method) {  // :168-19
         if (n_hat < (double)n) df1 = df_hat; else df0 = df_hat;
     }
     return df_hat;
+}
+
+// :389-419 (beta 4; kaiser() cannot fail here: index < length, beta >= 0)
+void orc_firdes_doppler(size_t n, double fd, double K, double theta, double* h) {
+    double beta = 4.0;
+    for (size_t i = 0; i < n; ++i) {
+        double t = (double)i - ((double)n - 1.0) / 2.0;
+        double j = 1.5 * besselj(std::fabs(2.0 * PI * fd * t), 0.0);
+        double r = 1.5 * K / (K + 1.0) * std::cos(2.0 * PI * fd * t * std::cos(theta));
+        double w = kaiser(i, n, beta);
+        h[i] = (j + r) * w;
+    }
+}
+double orc_filter_autocorrelation(const double* f, size_t n, long lag_s) {  // :443-456
+    size_t lag = lag_s < 0 ? (size_t)(-lag_s) : (size_t)lag_s;  // isize::unsigned_abs
+    if (lag >= n) return 0.0;
+    double rxx = 0.0;
+    for (size_t i = lag; i < n; ++i) rxx += f[i] * f[i - lag];
+    return rxx;
+}
+double orc_filter_crosscorrelation(const double* h, size_t nh, const double* g, size_t ng, long lag) {  // :487-527
+    if (nh < ng) return orc_filter_crosscorrelation(g, ng, h, nh, lag);
+    if (lag <= -(long)ng) return 0.0;
+    if (lag >= (long)nh) return 0.0;
+    size_t ig = 0, ih = 0;
+    if (lag < 0) ig = (size_t)(-lag);
+    if (lag > 0) ih = (size_t)lag;
+    long n;
+    if (lag < 0) n = (long)ng + lag;
+    else if (lag < (long)(nh - ng)) n = (long)ng;
+    else n = (long)nh - lag;
+    double rxy = 0.0;
+    for (size_t i = 0; i < (size_t)n; ++i) rxy += h[ih + i] * g[ig + i];
+    return rxy;
+}
+void orc_filter_isi(const double* f, size_t n, size_t sps, size_t delay, double* rms, double* mx) {  // :552-577
+    *rms = 0.0;
+    *mx = 0.0;
+    if (2 * sps * delay + 1 != n) return;
+    double rxx0 = orc_filter_autocorrelation(f, n, 0);
+    double isi_rms = 0.0, isi_max = 0.0;
+    for (size_t i = 1; i < 2 * delay; ++i) {
+        double e = std::fabs(orc_filter_autocorrelation(f, n, (long)(i * sps)) / rxx0);
+        isi_rms += e * e;
+        if (i == 1 || e > isi_max) isi_max = e;
+    }
+    *rms = std::sqrt(isi_rms / (2.0 * (double)delay));
+    *mx = isi_max;
+}
+// :602-640; 0 ok, 1 Bandwidth, 5 FilterSize, 6 FFTSize.  DotProduct<f64> FORWARD over
+// Complex<f64> samples: sum = 0; sum += c[k] * ejwt[k] (f64 * Complex: (c re, c im)).
+int orc_filter_energy(const double* f, size_t n, double fc, size_t fft_size, double* out) {
+    if (!(fc >= 0.0 && fc <= 0.5)) return 1;
+    if (n == 0) return 5;
+    if (fft_size == 0) return 6;
+    double e_total = 0.0, e_stopband = 0.0;
+    for (size_t i = 0; i < fft_size; ++i) {
+        double fr = 0.5 * (double)i / (double)fft_size;
+        double vr = 0.0, vi = 0.0;
+        for (size_t k = 0; k < n; ++k) {
+            double th = 2.0 * PI * fr * (double)k;
+            double er = 1.0 * std::cos(th), ei = 1.0 * std::sin(th);  // Complex::from_polar(1.0, th)
+            vr += f[k] * er;
+            vi += f[k] * ei;
+        }
+        double e2 = vr * vr - vi * (-vi);  // (v * v.conj()).re
+        e_total += e2;
+        if (fr > fc) e_stopband += e2;
+    }
+    *out = e_stopband / e_total;
+    return 0;
 }
 
 // src/filter/iirdes/pll/mod.rs:24-52 ; returns 0 ok, 1 bandwidth, 2 damping, 3 gain

@@ -1,5 +1,6 @@
 //! `solid::filter` (src/filter/mod.rs:1-22): the `Filter` trait, unchanged, and the
 //! device-backed filter types.
+pub mod auto_correlator;
 pub mod fir;
 pub mod firdes;
 pub mod iir;

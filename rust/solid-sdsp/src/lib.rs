@@ -1,11 +1,14 @@
 //! `solid` (juliantos/solid-dsp) streaming hot path on MI355X: the public types of
-//! `src/filter/*`, `src/dot_product/*` and `src/fft/*` with the same names and
+//! `src/filter/*`, `src/dot_product/*`, `src/fft/*`, `src/nco/*` and
+//! `src/auto_gain_control/*` with the same names and
 //! signatures (tests/test_rust_shim_api.py checks every `pub fn` against the
 //! reference), executed by libsdsp.so (include/sdsp.h).  Device-only extras are
 //! in `sdsp`.
+pub mod auto_gain_control;
 pub mod dot_product;
 pub mod fft;
 pub mod filter;
+pub mod nco;
 pub mod sdsp;
 pub mod sys;
 

@@ -8,6 +8,25 @@ use std::os::raw::{c_char, c_int, c_void};
 #[repr(C)] pub struct sdsp_iir { _p: [u8; 0] }
 #[repr(C)] pub struct sdsp_fft { _p: [u8; 0] }
 #[repr(C)] pub struct sdsp_chan { _p: [u8; 0] }
+#[repr(C)] pub struct sdsp_acorr { _p: [u8; 0] }
+#[repr(C)] pub struct sdsp_nco { _p: [u8; 0] }
+#[repr(C)] pub struct sdsp_agc { _p: [u8; 0] }
+
+/// struct AGC (auto_gain_control/mod.rs:96-108) as include/sdsp.h sdsp_agc_state
+#[repr(C)]
+#[derive(Clone, Copy, Default)]
+pub struct sdsp_agc_state {
+    pub gain: f64,
+    pub scale: f64,
+    pub bandwidth: f64,
+    pub alpha: f64,
+    pub energy_estimate: f64,
+    pub lock: i32,
+    pub squelch_mode: i32,
+    pub squelch_threshold: f64,
+    pub squelch_timeout: u64,
+    pub squelch_timer: u64,
+}
 
 pub const SDSP_RR32: c_int = 0;
 pub const SDSP_RC32: c_int = 1;
@@ -36,6 +55,12 @@ pub const SDSP_E_SOS_SIZE_MISMATCH: c_int = 13;
 pub const SDSP_E_SOS_SIZE_NOT_MULTIPLE_OF_3: c_int = 14;
 pub const SDSP_E_IIR_DECIMATION_LESS_THAN_ONE: c_int = 15;
 pub const SDSP_E_IIR_INTERPOLATION_LESS_THAN_ONE: c_int = 16;
+pub const SDSP_E_NCO_BANDWIDTH_OUT_OF_RANGE: c_int = 30;
+pub const SDSP_E_AGC_BANDWIDTH_OUT_OF_RANGE: c_int = 40;
+pub const SDSP_E_AGC_SIGNAL_LEVEL_OUT_OF_RANGE: c_int = 41;
+pub const SDSP_E_AGC_GAIN_BELOW_THRESHOLD: c_int = 42;
+pub const SDSP_E_AGC_SCALE_BELOW_THRESHOLD: c_int = 43;
+pub const SDSP_E_AGC_SAMPLES_TOO_LOW: c_int = 44;
 
 extern "C" {
     pub fn sdsp_last_error() -> *const c_char;
@@ -127,10 +152,75 @@ extern "C" {
 
     // tap / loop-filter design (firdes/mod.rs:243-368, iirdes/pll/mod.rs:24-99)
     pub fn sdsp_kaiser_beta(stop_band_attenuation: f64) -> f64;
+    // the rest of firdes (firdes/mod.rs:46-640); method 0 Kaiser, 1 Herrmann
+    pub fn sdsp_firdes_estimate_length(df: f64, as_: f64, method: c_int, len: *mut usize) -> c_int;
+    pub fn sdsp_firdes_estimate_length_kaiser(df: f64, as_: f64, len: *mut f64) -> c_int;
+    pub fn sdsp_firdes_estimate_length_herrmann(df: f64, as_: f64, len: *mut f64) -> c_int;
+    pub fn sdsp_firdes_estimate_stop_band_attenuation(df: f64, n: usize, method: c_int, as_: *mut f64) -> c_int;
+    pub fn sdsp_firdes_estimate_transition(as_: f64, n: usize, method: c_int, df: *mut f64) -> c_int;
+    pub fn sdsp_firdes_doppler(n: usize, fd: f64, k: f64, theta: f64, h: *mut f64) -> c_int;
+    pub fn sdsp_filter_autocorrelation(h: *const f64, n: usize, lag: isize) -> f64;
+    pub fn sdsp_filter_crosscorrelation(h: *const f64, nh: usize, g: *const f64, ng: usize, lag: isize) -> f64;
+    pub fn sdsp_filter_isi(h: *const f64, n: usize, sps: usize, delay: usize, rms: *mut f64, max: *mut f64) -> c_int;
+    pub fn sdsp_filter_energy(h: *const f64, n: usize, fc: f64, fft_size: usize, energy: *mut f64) -> c_int;
     pub fn sdsp_firdes_kaiser(n: usize, fc: f64, as_: f64, mu: f64, h: *mut f64) -> c_int;
     pub fn sdsp_firdes_notch(m: usize, f0: f64, as_: f64, h: *mut f64) -> c_int;
     pub fn sdsp_active_lag(bw: f64, zeta: f64, k: f64, num3: *mut f64, den3: *mut f64) -> c_int;
     pub fn sdsp_active_proportional_integral(bw: f64, zeta: f64, k: f64, num3: *mut f64, den3: *mut f64) -> c_int;
+
+    // AutoCorrelator (filter/auto_correlator/mod.rs:26-214); precision 0 Complex<f32>, 1 Complex<f64>
+    pub fn sdsp_acorr_create(out: *mut *mut sdsp_acorr, window_size: usize, delay: usize, precision: c_int,
+                             device: c_int) -> c_int;
+    pub fn sdsp_acorr_destroy(h: *mut sdsp_acorr);
+    pub fn sdsp_acorr_window_size(h: *const sdsp_acorr) -> usize;
+    pub fn sdsp_acorr_delay(h: *const sdsp_acorr) -> usize;
+    pub fn sdsp_acorr_reset(h: *mut sdsp_acorr) -> c_int;
+    pub fn sdsp_acorr_push(h: *mut sdsp_acorr, sample: *const c_void) -> c_int;
+    pub fn sdsp_acorr_write(h: *mut sdsp_acorr, samples: *const c_void, n: usize) -> c_int;
+    pub fn sdsp_acorr_execute(h: *mut sdsp_acorr, out: *mut c_void) -> c_int;
+    pub fn sdsp_acorr_execute_block(h: *mut sdsp_acorr, input: *const c_void, n: usize, out: *mut c_void) -> c_int;
+    pub fn sdsp_acorr_get_energy(h: *mut sdsp_acorr, energy: *mut f64) -> c_int;
+
+    // NCO (nco/mod.rs:27-187): u32 phase registers on the host, blocks mixed on the device
+    pub fn sdsp_nco_create(out: *mut *mut sdsp_nco, device: c_int) -> c_int;
+    pub fn sdsp_nco_destroy(h: *mut sdsp_nco);
+    pub fn sdsp_nco_reset(h: *mut sdsp_nco) -> c_int;
+    pub fn sdsp_nco_constrain(theta: f64) -> u32;
+    pub fn sdsp_nco_set_frequency(h: *mut sdsp_nco, delta_theta: f64) -> c_int;
+    pub fn sdsp_nco_adjust_frequency(h: *mut sdsp_nco, dt: f64) -> c_int;
+    pub fn sdsp_nco_get_frequency(h: *const sdsp_nco) -> f64;
+    pub fn sdsp_nco_set_phase(h: *mut sdsp_nco, phi: f64) -> c_int;
+    pub fn sdsp_nco_adjust_phase(h: *mut sdsp_nco, delta_phi: f64) -> c_int;
+    pub fn sdsp_nco_get_phase(h: *const sdsp_nco) -> f64;
+    pub fn sdsp_nco_step(h: *mut sdsp_nco) -> c_int;
+    pub fn sdsp_nco_sincos(h: *const sdsp_nco, sin_cos: *mut f64) -> c_int;
+    pub fn sdsp_nco_set_internal_pll_bandwidth(h: *mut sdsp_nco, bw: f64) -> c_int;
+    pub fn sdsp_nco_pll_step(h: *mut sdsp_nco, delta_phi: f64) -> c_int;
+    pub fn sdsp_nco_get_state(h: *const sdsp_nco, theta: *mut u32, delta_theta: *mut u32) -> c_int;
+    pub fn sdsp_nco_mix_block(h: *mut sdsp_nco, down: c_int, precision: c_int, input: *const c_void, n: usize,
+                              out: *mut c_void) -> c_int;
+
+    // AGC (auto_gain_control/mod.rs:97-677); sample_type 0 f64, 1 Complex<f64>
+    pub fn sdsp_agc_create(out: *mut *mut sdsp_agc, channels: usize, device: c_int) -> c_int;
+    pub fn sdsp_agc_destroy(h: *mut sdsp_agc);
+    pub fn sdsp_agc_reset(h: *mut sdsp_agc) -> c_int;
+    pub fn sdsp_agc_execute_block(h: *mut sdsp_agc, sample_type: c_int, input: *const c_void, n: usize,
+                                  out: *mut c_void) -> c_int;
+    pub fn sdsp_agc_init(h: *mut sdsp_agc, sample_type: c_int, input: *const c_void, n: usize,
+                         levels: *mut f64) -> c_int;
+    pub fn sdsp_agc_lock(h: *mut sdsp_agc) -> c_int;
+    pub fn sdsp_agc_unlock(h: *mut sdsp_agc) -> c_int;
+    pub fn sdsp_agc_set_bandwidth(h: *mut sdsp_agc, bandwidth: f64) -> c_int;
+    pub fn sdsp_agc_set_signal_level(h: *mut sdsp_agc, level: f64) -> c_int;
+    pub fn sdsp_agc_set_rssi(h: *mut sdsp_agc, rssi: f64) -> c_int;
+    pub fn sdsp_agc_set_gain(h: *mut sdsp_agc, gain: f64) -> c_int;
+    pub fn sdsp_agc_set_scale(h: *mut sdsp_agc, scale: f64) -> c_int;
+    pub fn sdsp_agc_update_squelch_mode(h: *mut sdsp_agc) -> c_int;
+    pub fn sdsp_agc_squelch_enable(h: *mut sdsp_agc) -> c_int;
+    pub fn sdsp_agc_squelch_disable(h: *mut sdsp_agc) -> c_int;
+    pub fn sdsp_agc_squelch_set_threshold(h: *mut sdsp_agc, threshold: f64) -> c_int;
+    pub fn sdsp_agc_squelch_set_timeout(h: *mut sdsp_agc, timeout: u64) -> c_int;
+    pub fn sdsp_agc_get_state(h: *mut sdsp_agc, channel: usize, st: *mut sdsp_agc_state) -> c_int;
 
     // DotProduct (dot_product/mod.rs:37-171)
     pub fn sdsp_dot_execute(dtype: c_int, coefs: *const c_void, len: usize, direction: c_int,

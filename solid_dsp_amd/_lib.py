@@ -130,6 +130,16 @@ def _declare(L):
         "sdsp_firdes_kaiser": (i, [sz, d, d, d, dp]),
         "sdsp_firdes_notch": (i, [sz, d, d, dp]),
         "sdsp_kaiser_beta": (d, [d]),
+        "sdsp_firdes_estimate_length": (i, [d, d, i, C.POINTER(sz)]),
+        "sdsp_firdes_estimate_length_kaiser": (i, [d, d, dp]),
+        "sdsp_firdes_estimate_length_herrmann": (i, [d, d, dp]),
+        "sdsp_firdes_estimate_stop_band_attenuation": (i, [d, sz, i, dp]),
+        "sdsp_firdes_estimate_transition": (i, [d, sz, i, dp]),
+        "sdsp_firdes_doppler": (i, [sz, d, d, d, dp]),
+        "sdsp_filter_autocorrelation": (d, [dp, sz, C.c_ssize_t]),
+        "sdsp_filter_crosscorrelation": (d, [dp, sz, dp, sz, C.c_ssize_t]),
+        "sdsp_filter_isi": (i, [dp, sz, sz, sz, dp, dp]),
+        "sdsp_filter_energy": (i, [dp, sz, d, sz, dp]),
         "sdsp_active_lag": (i, [d, d, d, dp, dp]),
         "sdsp_active_proportional_integral": (i, [d, d, d, dp, dp]),
         "sdsp_fir_group_delay_taps": (i, [dp, sz, d, dp]),
@@ -212,6 +222,7 @@ def _optional_sigs():
         "sdsp_nco_create": (i, [vpp, i]),
         "sdsp_nco_destroy": (None, [vp]),
         "sdsp_nco_reset": (i, [vp]),
+        "sdsp_nco_constrain": (C.c_uint32, [d]),
         "sdsp_nco_set_frequency": (i, [vp, d]),
         "sdsp_nco_adjust_frequency": (i, [vp, d]),
         "sdsp_nco_get_frequency": (d, [vp]),
@@ -241,6 +252,7 @@ def _optional_sigs():
         "sdsp_agc_set_rssi": (i, [vp, d]),
         "sdsp_agc_set_gain": (i, [vp, d]),
         "sdsp_agc_set_scale": (i, [vp, d]),
+        "sdsp_agc_update_squelch_mode": (i, [vp]),
         "sdsp_agc_squelch_enable": (i, [vp]),
         "sdsp_agc_squelch_disable": (i, [vp]),
         "sdsp_agc_squelch_set_threshold": (i, [vp, d]),

@@ -185,6 +185,9 @@ class AGC:
     def squelch_set_timeout(self, timeout: int):
         L.check(L.lib().sdsp_agc_squelch_set_timeout(self._h, int(timeout)))
 
+    def update_squelch_mode(self):  # :631-677 (one step per channel)
+        L.check(L.lib().sdsp_agc_update_squelch_mode(self._h))
+
     def squelch_get_mode(self) -> SquelchMode:
         return SquelchMode(self.state().squelch_mode)
 

@@ -267,9 +267,19 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         Fa[0] = f2{e1.z, e1.w}, Fa[1] = f2{e2.x, e2.y}, Fa[2] = f2{e2.z, e2.w};
     }
     f2* col = img + t + (t >> 4);  // (r, t) at col[r * kRow]
+    // the fused DFT16 (72 instead of 81 packed instructions, sdsp_pk.hpp: 3.112 -> 3.056 ms sustained,
+    // profiles/r06/lab/r06b_olsab.log); 67108864 the round-5 DFT16 (lab)
+    auto dft = [](f2(&w)[16]) {
+        if constexpr ((ABL & 67108864) != 0) pdft16<false>(w);
+        else pdft16f<false>(w);
+    };
+    auto idft = [](f2(&w)[16]) {
+        if constexpr ((ABL & 67108864) != 0) pdft16<true>(w);
+        else pdft16f<true>(w);
+    };
 
     // P1: DFT16 n2 -> k0, * W4096^(t k0) -> (k0, t)
-    pdft16<false>(v);
+    dft(v);
 #pragma unroll
     for (int k = 0; k < 16; ++k) col[k * kRow] = k == 0 ? v[0] : pmul(v[kout(k)], tw_pair(Cb, Da, k));
     __syncthreads();
@@ -287,7 +297,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     f2 w2[16];  // W256^(lo4 k), used by P2 (n0 = lo4) and P3 (k1 = lo4)
 #pragma unroll
     for (int k = 1; k < 16; ++k) w2[k] = tw_pair(Eb, Fa, k);
-    pdft16<false>(v);
+    dft(v);
 #pragma unroll
     for (int k = 0; k < 16; ++k) r2[17 * k] = k == 0 ? v[0] : pmul(v[kout(k)], w2[k]);
     phase_sync<!(ABL & 1)>();
@@ -297,14 +307,14 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         f2* r3 = img + hi4 * kRow + 17 * lo4;  // (hi4, 16 lo4 + j) at r3[j]
 #pragma unroll
         for (int j = 0; j < 16; ++j) v[j] = r3[j];
-        pdft16<false>(v);
+        dft(v);
         f2 u[16];
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
             u[2 * p] = pmul(v[kout(2 * p)], f2{hq[p].x, hq[p].y});
             u[2 * p + 1] = pmul(v[kout(2 * p + 1)], f2{hq[p].z, hq[p].w});
         }
-        pdft16<true>(u);
+        idft(u);
 #pragma unroll
         for (int j = 0; j < 16; ++j) r3[j] = j == 0 ? u[kout(0)] : pmulc(u[kout(j)], w2[j]);
     }
@@ -313,7 +323,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     // P4: lane (k0 = hi4, n0 = lo4): IDFT16 k1 -> n1 -> (k0, 16 n1 + n0)
 #pragma unroll
     for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
-    pdft16<true>(v);
+    idft(v);
 #pragma unroll
     for (int k = 0; k < 16; ++k) r2[17 * k] = v[kout(k)];
     __syncthreads();
@@ -324,7 +334,7 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     for (int i = 0; i < 3; ++i) asm volatile("" : "+v"(Cb[i]), "+v"(Da[i]));
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = k == 0 ? col[0] : pmulc(col[k * kRow], tw_pair(Cb, Da, k));
-    pdft16<true>(v);
+    idft(v);
     if constexpr (ABL & 2) {  // outputs kept live, not stored
         f2 acc = v[0];
 #pragma unroll

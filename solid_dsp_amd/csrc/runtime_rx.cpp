@@ -328,6 +328,7 @@ int sdsp_nco_reset(sdsp_nco* h) {  // :53-56
     h->delta_theta = 0;
     return SDSP_OK;
 }
+uint32_t sdsp_nco_constrain(double theta) { return constrain(theta); }  // :175-187
 int sdsp_nco_set_frequency(sdsp_nco* h, double dtheta) {  // :59-61
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     h->delta_theta = constrain(dtheta);
@@ -654,6 +655,29 @@ int sdsp_agc_set_scale(sdsp_agc* h, double scale) {  // :535-542
         return h ? SDSP_E_AGC_SCALE_BELOW_THRESHOLD : SDSP_E_INVALID_ARGUMENT;
     }
     return agc_update(h, [scale](sdsp_agc_state& s) { s.scale = scale; });
+}
+// update_squelch_mode  :631-677 (one step of the state machine per channel, as execute makes it)
+int sdsp_agc_update_squelch_mode(sdsp_agc* h) {
+    return agc_update(h, [](sdsp_agc_state& s) {
+        const bool hi = std::log10(s.gain) * -20.0 > s.squelch_threshold;  // get_rssi() > threshold
+        switch (s.squelch_mode) {
+            case SDSP_SQUELCH_ENABLED: s.squelch_mode = hi ? SDSP_SQUELCH_RISE : SDSP_SQUELCH_ENABLED; break;
+            case SDSP_SQUELCH_RISE: s.squelch_mode = hi ? SDSP_SQUELCH_SIGNALHI : SDSP_SQUELCH_FALL; break;
+            case SDSP_SQUELCH_SIGNALHI: s.squelch_mode = hi ? SDSP_SQUELCH_SIGNALHI : SDSP_SQUELCH_FALL; break;
+            case SDSP_SQUELCH_FALL:
+                s.squelch_timer = s.squelch_timeout;
+                s.squelch_mode = hi ? SDSP_SQUELCH_SIGNALHI : SDSP_SQUELCH_SIGNALLO;
+                break;
+            case SDSP_SQUELCH_SIGNALLO:
+                s.squelch_timer -= 1;  // usize: wraps in release builds
+                s.squelch_mode = s.squelch_timer == 0 ? SDSP_SQUELCH_TIMEOUT
+                                 : hi                 ? SDSP_SQUELCH_SIGNALHI
+                                                      : SDSP_SQUELCH_SIGNALLO;
+                break;
+            case SDSP_SQUELCH_TIMEOUT: s.squelch_mode = SDSP_SQUELCH_ENABLED; break;
+            default: s.squelch_mode = SDSP_SQUELCH_DISABLED; break;
+        }
+    });
 }
 int sdsp_agc_squelch_enable(sdsp_agc* h) {
     return agc_update(h, [](sdsp_agc_state& s) { s.squelch_mode = SDSP_SQUELCH_ENABLED; });

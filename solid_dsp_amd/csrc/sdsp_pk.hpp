@@ -109,5 +109,53 @@ template <bool INV> __device__ __forceinline__ void pdft16(f2 (&v)[16]) {
     for (int ka = 0; ka < 4; ++ka) pdft4<INV>(v[4 * ka + 0], v[4 * ka + 1], v[4 * ka + 2], v[4 * ka + 3]);
 }
 
+// ---- the fused DFT16 of the one-shot overlap-save kernel (kern_fir_ols_os.hip) ----
+// R = -j (forward) / +j (inverse), the DFT4 rotation.  x + k R y as one v_pk_fma_f32.
+template <bool INV> __device__ __forceinline__ f2 rfma(f2 y, float k, f2 x) {
+    return __builtin_elementwise_fma(y.yx, INV ? f2{-k, k} : f2{k, -k}, x);
+}
+constexpr float kT1 = 0.41421356237309505f;  // tan(pi/8)
+
+// the same DFT16 as pdft16 (natural order in, stage order out) in 72 instead of 81 packed
+// instructions: the second-stage twiddles are written W1 = c1 (1 + t R), W3 = c1 R (1 - t R),
+// W2 = r2 (1 + R), W6 = r2 R (1 + R), W9 = -W1 (c1 = cos pi/8, t = tan pi/8, r2 = sqrt 1/2),
+// so each twiddled input costs one fma and its real scale folds into the DFT4's sums.  Equal to
+// pdft16 within rounding (not bit for bit).
+template <bool INV> __device__ __forceinline__ void pdft16f(f2 (&v)[16]) {
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) pdft4<INV>(v[nb], v[4 + nb], v[8 + nb], v[12 + nb]);
+    pdft4<INV>(v[0], v[1], v[2], v[3]);
+    const f2 c1 = {kC1, kC1}, nc1 = {-kC1, -kC1}, r2 = {kR2, kR2}, nr2 = {-kR2, -kR2};
+    {  // ka = 1: W1, W2, W3
+        const f2 g1 = rfma<INV>(v[5], kT1, v[5]), g3 = rfma<INV>(v[7], -kT1, v[7]);
+        const f2 cc = rfma<INV>(g3, 1.0f, g1), ee = rfma<INV>(g3, -1.0f, g1);
+        const f2 u2 = rfma<INV>(v[6], 1.0f, v[6]);
+        const f2 a = __builtin_elementwise_fma(u2, r2, v[4]), b = __builtin_elementwise_fma(u2, nr2, v[4]);
+        v[4] = __builtin_elementwise_fma(cc, c1, a);
+        v[6] = __builtin_elementwise_fma(cc, nc1, a);
+        v[5] = rfma<INV>(ee, kC1, b);
+        v[7] = rfma<INV>(ee, -kC1, b);
+    }
+    {  // ka = 2: W2, W4 = R, W6
+        const f2 a = rfma<INV>(v[10], 1.0f, v[8]), b = rfma<INV>(v[10], -1.0f, v[8]);
+        const f2 p = rfma<INV>(v[11], 1.0f, v[9]), q = rfma<INV>(v[11], -1.0f, v[9]);
+        const f2 u = rfma<INV>(p, 1.0f, p), s = rfma<INV>(q, 1.0f, q);
+        v[8] = __builtin_elementwise_fma(u, r2, a);
+        v[10] = __builtin_elementwise_fma(u, nr2, a);
+        v[9] = rfma<INV>(s, kR2, b);
+        v[11] = rfma<INV>(s, -kR2, b);
+    }
+    {  // ka = 3: W3, W6, W9
+        const f2 h1 = rfma<INV>(v[13], -kT1, v[13]), h3 = rfma<INV>(v[15], kT1, v[15]);
+        const f2 cc = rfma<INV>(h1, 1.0f, -h3), ee = rfma<INV>(h1, 1.0f, h3);
+        const f2 u2 = rfma<INV>(v[14], 1.0f, v[14]);
+        const f2 a = rfma<INV>(u2, kR2, v[12]), b = rfma<INV>(u2, -kR2, v[12]);
+        v[12] = __builtin_elementwise_fma(cc, c1, a);
+        v[14] = __builtin_elementwise_fma(cc, nc1, a);
+        v[13] = rfma<INV>(ee, kC1, b);
+        v[15] = rfma<INV>(ee, -kC1, b);
+    }
+}
+
 }  // namespace pk
 }  // namespace sdsp

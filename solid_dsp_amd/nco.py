@@ -17,6 +17,10 @@ import numpy as np
 from . import _lib as L
 
 
+def constrain(theta: float) -> int:  # :175-187 (the u32 phase of an angle)
+    return int(L.lib().sdsp_nco_constrain(float(theta)))
+
+
 class NCOError(L.SdspError):
     """NCOError(NCOErrorCode::BandwidthOutOfRange)  (src/nco/mod.rs:7-24)."""
 

@@ -3,6 +3,9 @@
 
 * butter8_0p2_sos.json -- cfg3's 4-section cascade, scipy.signal.butter(8, 0.2,
   output='sos'), rows [b0 b1 b2 a0 a1 a2].
+* butter8_0p01_sos.json -- a narrow-band cascade, scipy.signal.butter(8, 0.01,
+  output='sos'): section 0 carries the whole gain (b0 = 3.4e-15), the case the
+  wave scan's b0-factored coordinates scale states by ~1/b0 (test_gpu_iir.py).
 * vectors_*.npz -- make_vectors(): inputs and expected outputs for the rows the
   reference's own tests do not pin (PolyPhaseFilterBank, InterpolatingFIRFilter,
   the channeliser, FFT, full-complex FIR), computed by the oracle restatement
@@ -26,9 +29,10 @@ SEED = 20250226
 
 def make_butter():
     from scipy import signal
-    sos = signal.butter(8, 0.2, output="sos")
-    with open(os.path.join(HERE, "butter8_0p2_sos.json"), "w") as f:
-        json.dump({"source": "scipy.signal.butter(8, 0.2, output='sos')", "sos": sos.tolist()}, f, indent=1)
+    for wn, name in ((0.2, "butter8_0p2_sos.json"), (0.01, "butter8_0p01_sos.json")):
+        sos = signal.butter(8, wn, output="sos")
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump({"source": "scipy.signal.butter(8, %g, output='sos')" % wn, "sos": sos.tolist()}, f, indent=1)
 
 
 def _rand(rng, n, dt):

@@ -76,6 +76,11 @@ def lib():
         "orc_estimate_req_filter_len": (C.c_int, [C.c_double, C.c_double, C.c_int, C.POINTER(sz)]),
         "orc_estimate_req_filter_as": (C.c_double, [C.c_double, sz, C.c_int]),
         "orc_estimate_req_filter_df": (C.c_double, [C.c_double, sz, C.c_int]),
+        "orc_firdes_doppler": (None, [sz, C.c_double, C.c_double, C.c_double, dp]),
+        "orc_filter_autocorrelation": (C.c_double, [dp, sz, C.c_long]),
+        "orc_filter_crosscorrelation": (C.c_double, [dp, sz, dp, sz, C.c_long]),
+        "orc_filter_isi": (None, [dp, sz, sz, sz, dp, dp]),
+        "orc_filter_energy": (C.c_int, [dp, sz, C.c_double, sz, dp]),
         "orc_active_lag": (C.c_int, [C.c_double, C.c_double, C.c_double, dp, dp]),
         "orc_active_pi": (C.c_int, [C.c_double, C.c_double, C.c_double, dp, dp]),
         "orc_synth_f32": (None, [C.c_uint64, C.c_uint64, C.c_uint64, sz, C.POINTER(C.c_float)]),

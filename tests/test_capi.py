@@ -65,6 +65,71 @@ def test_host_design_matches_oracle():
         firdes.firdes_kaiser(8, 0.7, 60.0)
 
 
+def test_firdes_full_set_matches_oracle_and_kats():
+    """VERDICT r05 missing #2: the rest of solid::filter::firdes (src/filter/firdes/mod.rs:46-640)
+    in the product's design.cpp -- bit-equal to the oracle restatement on a sweep of arguments, the
+    reference's doctest KATs through libsdsp.so, and the reference's error codes."""
+    import oracle_lib as O
+    from solid_dsp_amd.filter import firdes as F
+    L = O.lib()
+    M = F.EstimationMethod
+    # KATs (doctests :64-69, :110-115, :161-166, :431-441, :470-485, :540-550, :589-600)
+    assert F.estimate_required_filter_length(0.35, 100.0, M.Herrmann) == 15
+    assert int(F.estimate_required_filter_stop_band_attenuation(0.35, 16, M.Herrmann)) == 101
+    assert int((F.estimate_required_filter_transition(101.0, 16, M.Herrmann) + 0.005) * 100.0) == 35
+    assert len(F.firdes_doppler(51, 0.1, 2.0, 0.0)) == 51
+    h = F.firdes_notch(25, 0.2, 30.0)
+    assert F.filter_autocorrelation(h, 3) == F.filter_autocorrelation(h, -3)
+    assert np.float32(F.filter_autocorrelation(h, 3)) == np.float32(0.047983058)
+    k = F.firdes_kaiser(51, 0.35, 120.0, 0.0)
+    assert np.float32(F.filter_crosscorrelation(k, h, 0)) == np.float32(0.92825377)
+    rms, mx = F.filter_isi(h, 1, 25)
+    assert np.float32(rms) == np.float32(0.02509764) and np.float32(mx) == np.float32(0.061966006)
+    assert np.float32(F.filter_energy(h, 0.35, 128)) == np.float32(0.3152318)
+    # bit equality with the restatement
+    for method in (M.Kaiser, M.Herrmann):
+        for df, as_ in [(0.35, 100.0), (0.05, 60.0), (0.2, 120.0), (0.01, 30.0), (0.5, 106.0)]:
+            out = O.C.c_size_t(0)
+            assert L.orc_estimate_req_filter_len(df, as_, int(method), O.C.byref(out)) == 0
+            assert F.estimate_required_filter_length(df, as_, method) == out.value
+        for df, n in [(0.35, 16), (0.1, 63), (0.02, 256)]:
+            assert F.estimate_required_filter_stop_band_attenuation(df, n, method) == \
+                L.orc_estimate_req_filter_as(df, n, int(method))
+        for as_, n in [(101.0, 16), (60.0, 63), (80.0, 256)]:
+            assert F.estimate_required_filter_transition(as_, n, method) == L.orc_estimate_req_filter_df(as_, n, int(method))
+    for args in [(51, 0.1, 2.0, 0.0), (64, 0.03, 0.5, 0.7), (7, 0.25, 10.0, 1.2), (1, 0.1, 2.0, 0.0)]:
+        ref = np.zeros(args[0])
+        L.orc_firdes_doppler(*args, O._dptr(ref))
+        assert np.array_equal(F.firdes_doppler(*args), ref, equal_nan=True), args
+    g = F.firdes_kaiser(20, 0.2, 60.0, 0.0)
+    for lag in (-60, -51, -50, -19, -3, 0, 1, 7, 31, 32, 50, 51, 80):
+        assert F.filter_autocorrelation(k, lag) == L.orc_filter_autocorrelation(O._dptr(k), len(k), lag)
+        for a, b in ((k, g), (g, k), (h, k)):
+            assert F.filter_crosscorrelation(a, b, lag) == \
+                L.orc_filter_crosscorrelation(O._dptr(a), len(a), O._dptr(b), len(b), lag), (len(a), len(b), lag)
+    for sps, delay in ((1, 25), (2, 12), (5, 5), (3, 3)):
+        rr, rm = O.C.c_double(0), O.C.c_double(0)
+        L.orc_filter_isi(O._dptr(h), len(h), sps, delay, O.C.byref(rr), O.C.byref(rm))
+        assert F.filter_isi(h, sps, delay) == (rr.value, rm.value)
+    for fc, nfft in ((0.35, 128), (0.1, 64), (0.0, 7), (0.5, 33)):
+        e = O.C.c_double(0)
+        assert L.orc_filter_energy(O._dptr(k), len(k), fc, nfft, O.C.byref(e)) == 0
+        assert F.filter_energy(k, fc, nfft) == e.value
+    # FirdesErrorCode (firdes/mod.rs:17-44): Bandwidth, StopBandLevel, FilterSize, FFTSize
+    for call, code in [(lambda: F.estimate_required_filter_length(0.6, 60.0, M.Kaiser), 1),
+                       (lambda: F.estimate_required_filter_length(0.2, 0.0, M.Herrmann), 2),
+                       (lambda: F.estimate_required_filter_length_kaiser(-0.1, 60.0), 1),
+                       (lambda: F.estimate_required_filter_length_herrmann(0.1, -1.0), 2),
+                       (lambda: F.estimate_required_filter_stop_band_attenuation(0.7, 16, M.Kaiser), 1),
+                       (lambda: F.estimate_required_filter_transition(-5.0, 16, M.Herrmann), 2),
+                       (lambda: F.filter_energy(h, 0.6, 128), 1),
+                       (lambda: F.filter_energy([], 0.2, 128), 5),
+                       (lambda: F.filter_energy(h, 0.2, 0), 6)]:
+        with pytest.raises(F.FirdesError) as e:
+            call()
+        assert e.value.code == code
+
+
 def test_cfg5_prototype_design_is_finite():
     from solid_dsp_amd.filter import firdes
     h = firdes.firdes_kaiser(8192, 1 / 2048, 80.0, 0.0)

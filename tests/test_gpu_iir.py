@@ -559,3 +559,139 @@ def test_iir_time_shard_exchange_on_device():
         s_zero = A @ s_zero + b * float(xs[k])
     s_ref = st + s_zero
     assert np.linalg.norm(s_end - s_ref) <= 1e-5 * max(np.linalg.norm(s_ref), 1.0)
+
+
+# ---------------------------------------------------------------- b0-factored wave-scan edges
+def narrow_butter():
+    sos = np.array(json.load(open(os.path.join(HERE, "golden", "butter8_0p01_sos.json")))["sos"])
+    return sos[:, :3].reshape(-1), sos[:, 3:].reshape(-1)
+
+
+def _f64_ref(sdt, ff, fb, state=None):
+    o = O.iir(O.RC64 if np.dtype(sdt).kind == "c" else O.RR64, ff.astype(np.float64), fb.astype(np.float64),
+              O.SECOND_ORDER)
+    if state is not None:
+        o.sos_state(np.asarray(state).astype(o.in_dt))
+    return o
+
+
+def _wide(x):
+    return x.astype(np.complex128 if x.dtype.kind == "c" else np.float64)
+
+
+def _state_close(st, ref, tol):
+    """per section (w1, w2): the reference's units, relative to that section's own magnitude"""
+    st, ref = np.asarray(st).reshape(-1, 2), np.asarray(ref).reshape(-1, 2)
+    for q in range(ref.shape[0]):
+        scale = max(np.linalg.norm(ref[q]), 1e-300)
+        assert np.linalg.norm(st[q] - ref[q]) <= tol * scale, (q, st[q], ref[q])
+
+
+def shifted_butter(k):
+    """cfg3's butter(8, 0.2) with the gain moved: section 0's numerator times 10^-k, the last
+    section's times 10^k (the same transfer function; b0 of section 0 = 2.4e-5 * 10^-k)"""
+    ff, fb = butter()
+    ff = ff.copy()
+    ff[:3] *= 10.0 ** -k
+    ff[-3:] *= 10.0 ** k
+    return ff, fb
+
+
+TINY_B0 = [  # (cascade, whether it must take the wave scan)
+    ("shifted12", True),   # b0 = 2.4e-17 in section 0: states of sections 1..3 run at ~4e16 x
+    ("narrow", None),      # butter(8, 0.01): b0 = 3.4e-15, poles at |z| = 0.994 (any path)
+]
+
+
+@pytest.mark.parametrize("dt,cdt,sdt,tol", [(O.RR32, np.float32, np.float32, 1e-5),
+                                            (O.RC32, np.float32, np.complex64, 1e-5),
+                                            (O.RR64, np.float64, np.float64, 1e-12)])
+@pytest.mark.parametrize("case,wave", TINY_B0)
+def test_wave_scan_tiny_leading_b0(dt, cdt, sdt, tol, case, wave):
+    """VERDICT r05 weak #1 / ADVICE r05: a cascade whose section 0 holds a tiny b0 makes the wave
+    scan's b0-factored coordinates (runtime_iir.cpp wscan_coefs) run sections 1..3 on states divided
+    by G = b0 -- 1e14..1e17 times the reference's values in f32.  The gain-shifted cfg3 cascade must
+    take the wave scan (butter(8, 0.01) may not: its slow poles keep f32 off it, and it is checked
+    on whichever path it takes), meet the scan tolerance against the f64 restatement
+    (sos.rs:92-114 per section) over ragged calls, report its state in the reference's units
+    (get_state vs the restatement's (w1, w2) per section), and round-trip that state into a serial
+    handle and back (set_state on a wave-scan handle from the reference-order loop's state)."""
+    ff, fb = shifted_butter(12) if case == "shifted12" else narrow_butter()
+    ff, fb = ff.astype(cdt), fb.astype(cdt)
+    f = IIRFilter(ff, fb, SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    if wave:
+        assert f.wscan_mode() in (1, 2)
+    mode = f.wscan_mode()
+    n = 300001
+    x = O.synth(20250301, 1, 0, n, complex_=np.dtype(sdt).kind == "c").astype(sdt)
+    cuts = [0, 7, 70000, 70001, 200000, n]
+    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(cuts, cuts[1:])])
+    o = _f64_ref(sdt, ff, fb)
+    ref = o.execute_block(_wide(x))
+    if cdt == np.float32:  # no better than the f32 reference-order loop allows, both against f64
+        tol = max(tol, 10 * rel_rms(O.iir(dt, ff, fb, O.SECOND_ORDER).execute_block(x), ref))
+    assert rel_rms(y, ref) <= tol, (rel_rms(y, ref), tol)
+    assert np.abs(y - ref).max() <= 10 * tol * np.abs(ref).max()
+    st, _ = f.get_state()
+    _state_close(st, o.sos_state(), 10 * tol)
+    # the wave scan's state into the reference-order loop: bit-identical to the restatement at the
+    # handle's precision continued from that state
+    m = 50000
+    z = O.synth(20250302, 1, 0, m, complex_=np.dtype(sdt).kind == "c").astype(sdt)
+    g = IIRFilter(ff, fb, SO, sample_dtype=sdt, algo=sd.ALGO_EXACT)
+    g.set_state(st)
+    oz = O.iir(dt, ff, fb, O.SECOND_ORDER)
+    oz.sos_state(st)
+    assert bits_equal(g.execute_block(z), oz.execute_block(z))
+    # and a serial state into the wave-scan handle: the f64 restatement from the same state
+    sg, _ = g.get_state()
+    f.set_state(sg)
+    o2 = _f64_ref(sdt, ff, fb, sg)
+    x2 = O.synth(20250303, 1, 0, 2 * m, complex_=np.dtype(sdt).kind == "c").astype(sdt)
+    y2 = f.execute_block(x2)
+    assert f.wscan_mode() == mode
+    ref2 = o2.execute_block(_wide(x2))
+    assert rel_rms(y2, ref2) <= tol, (rel_rms(y2, ref2), tol)
+    _state_close(f.get_state()[0], o2.sos_state(), 10 * tol)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt,tol", [(O.RR32, np.float32, np.float32, 1e-5),
+                                            (O.RR64, np.float64, np.float64, 1e-12),
+                                            (O.RC64, np.float64, np.complex128, 1e-12)])
+@pytest.mark.parametrize("case", ["zero_b0", "scale_out_of_range"])
+def test_zero_b0_section_leaves_wave_scan(dt, cdt, sdt, tol, case):
+    """A cascade whose first (non-last) section has b0 = 0 has no b0-factored form
+    (runtime_iir.cpp wscan_coefs returns false): the group must leave the wave scan
+    (wscan_mode 0) and still meet parity on the block scan, with get_state / set_state
+    round trips in the reference's units (sos.rs:55-114).  The same for a cascade whose scale
+    G = prod b0 leaves [1e-30, 1e30] (cfg3's butter with 10^-40 moved into section 0, f64 only)."""
+    if case == "zero_b0":
+        ff = np.array([0.0, 1.0, 0.5, 0.2, 0.4, 0.2], dtype=cdt)
+        fb = np.array([1.0, -0.5, 0.1, 1.0, -1.2, 0.5], dtype=cdt)
+    else:
+        if cdt == np.float32:
+            pytest.skip("10^-40 is below the f32 range")
+        ff, fb = (c.astype(cdt) for c in shifted_butter(40))
+    f = IIRFilter(ff, fb, SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    assert f.wscan_mode() == 0
+    n = 200001
+    x = O.synth(20250304, 2, 0, n, complex_=np.dtype(sdt).kind == "c").astype(sdt)
+    cuts = [0, 5, 9000, 120000, n]
+    y = np.concatenate([f.execute_block(x[a:b]) for a, b in zip(cuts, cuts[1:])])
+    o = _f64_ref(sdt, ff, fb)
+    ref = o.execute_block(_wide(x))
+    assert rel_rms(y, ref) <= tol, rel_rms(y, ref)
+    assert np.abs(y - ref).max() <= tol * np.abs(ref).max()
+    st, _ = f.get_state()
+    _state_close(st, o.sos_state(), 10 * tol)
+    g = IIRFilter(ff, fb, SO, sample_dtype=sdt, algo=sd.ALGO_EXACT)
+    g.set_state(st)
+    oz = O.iir(dt, ff, fb, O.SECOND_ORDER)
+    oz.sos_state(st)
+    z = x[:30000]
+    assert bits_equal(g.execute_block(z), oz.execute_block(z))
+    f.set_state(g.get_state()[0])
+    o2 = _f64_ref(sdt, ff, fb, g.get_state()[0])
+    y2 = f.execute_block(x[30000:150000])
+    ref2 = o2.execute_block(_wide(x[30000:150000]))
+    assert rel_rms(y2, ref2) <= tol

@@ -1,5 +1,5 @@
-"""The reference's doctests of the hot path (juliantos/solid-dsp src/filter/{fir,iir}/*.rs,
-src/dot_product/*.rs), translated statement by statement by tools/port_doctests.py to the
+"""The reference's doctests of the hot path (juliantos/solid-dsp src/filter/{fir,iir,firdes}/*.rs,
+src/filter/auto_correlator, src/dot_product/*.rs, src/nco, src/auto_gain_control), translated statement by statement by tools/port_doctests.py to the
 Python mirror of the C ABI (solid_dsp_amd) and run on the MI355X: every call goes through
 libsdsp.so, and each asserted literal is the reference's, compared exactly as Rust's
 assert_eq! compares (f64 / Complex<f64> equality).  Generated -- edit the porter, not this file."""
@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 sd = pytest.importorskip("solid_dsp_amd")
 from solid_dsp_amd import (FIRFilter, DecimatingFIRFilter, InterpolatingFIRFilter, PolyPhaseFilterBank,  # noqa
                            IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter, InterpolatingIIRFilter,
-                           DotProduct, Direction)
+                           DotProduct, Direction, AGC, NCO, AutoCorrelator)
 from solid_dsp_amd.filter import firdes, iirdes  # noqa: E402
 from solid_dsp_amd.filter.firdes import *  # noqa: E402,F401,F403
 
@@ -562,3 +562,322 @@ def test_dot_product_execute_l7():
     mul = [1.0] * 5
     exe = dp.execute(mul)
     _eq(exe, 15.0)
+
+
+def test_filter_firdes_mod_l61():
+    """src/filter/firdes/mod.rs:61"""
+    est = estimate_required_filter_length(0.35, 100.0, EstimationMethod.Herrmann)
+    _eq(est, 15)
+
+
+def test_filter_firdes_mod_l107():
+    """src/filter/firdes/mod.rs:107"""
+    est = estimate_required_filter_stop_band_attenuation(0.35, 16, EstimationMethod.Herrmann)
+    _eq(int(est), 101)
+
+
+def test_filter_firdes_mod_l158():
+    """src/filter/firdes/mod.rs:158"""
+    est = (lambda est: (est + 0.005) * 100.0)(estimate_required_filter_transition(101.0, 16, EstimationMethod.Herrmann))
+    _eq(int(est), 35)
+
+
+def test_filter_firdes_mod_l268():
+    """src/filter/firdes/mod.rs:268"""
+    taps = firdes.firdes_kaiser(8, 0.35, 120.0, 0.0)
+    _eq(_len(taps), 8)
+
+
+def test_filter_firdes_mod_l319():
+    """src/filter/firdes/mod.rs:319"""
+    taps = firdes.firdes_notch(8, 0.35, 120.0)
+    _eq(_len(taps), 17)
+
+
+def test_filter_firdes_mod_l379():
+    """src/filter/firdes/mod.rs:379"""
+    taps = firdes.firdes_doppler(51, 0.1, 2.0, 0.0)
+    _eq(_len(taps), 51)
+
+
+def test_filter_firdes_mod_l429():
+    """src/filter/firdes/mod.rs:429"""
+    taps = firdes_notch(25, 0.2, 30.0)
+    auto_corr = filter_autocorrelation(taps, 3)
+    rev_auto_corr = filter_autocorrelation(taps, -3)
+    _eq(auto_corr, rev_auto_corr)
+    _eq(np.float32(auto_corr), np.float32(0.047983058))
+
+
+def test_filter_firdes_mod_l470():
+    """src/filter/firdes/mod.rs:470"""
+    h = firdes_kaiser(51, 0.35, 120.0, 0.0)
+    g = firdes_notch(25, 0.20, 30.0)
+    cross_corr = filter_crosscorrelation(h, g, 0)
+    _eq(np.float32(cross_corr), np.float32(0.92825377))
+
+
+def test_filter_firdes_mod_l539():
+    """src/filter/firdes/mod.rs:539"""
+    h = firdes_notch(25, 0.20, 30.0)
+    rms, max = filter_isi(h, 1, 25)
+    _eq(np.float32(rms), np.float32(0.02509764))
+    _eq(np.float32(max), np.float32(0.061966006))
+
+
+def test_filter_firdes_mod_l588():
+    """src/filter/firdes/mod.rs:588"""
+    h = firdes_notch(25, 0.20, 30.0)
+    energy = filter_energy(h, 0.35, 128)
+    _eq(np.float32(energy), np.float32(0.3152318))
+
+
+def test_filter_auto_correlator_mod_l7():
+    """src/filter/auto_correlator/mod.rs:7"""
+    auto_corr_filter = AutoCorrelator(10, 5, dtype=np.complex128)
+
+
+def test_filter_auto_correlator_mod_l46():
+    """src/filter/auto_correlator/mod.rs:46"""
+    auto_corr_filter = AutoCorrelator(10, 5, dtype=np.complex128)
+
+
+def test_filter_auto_correlator_mod_l68():
+    """src/filter/auto_correlator/mod.rs:68"""
+    auto_corr = AutoCorrelator(10, 5, dtype=np.complex128)
+    auto_corr.push(complex(4.0, 0.0))
+    auto_corr.reset()
+
+
+def test_filter_auto_correlator_mod_l92():
+    """src/filter/auto_correlator/mod.rs:92"""
+    auto_corr = AutoCorrelator(5, 10, dtype=np.complex128)
+    auto_corr.push(complex(4.0, 0.0))
+
+
+def test_filter_auto_correlator_mod_l120():
+    """src/filter/auto_correlator/mod.rs:120"""
+    auto_corr = AutoCorrelator(5, 10, dtype=np.complex128)
+    window = [complex(2.02, 0.0), complex(4.04, 0.0)]
+    auto_corr.write(window)
+
+
+def test_filter_auto_correlator_mod_l143():
+    """src/filter/auto_correlator/mod.rs:143"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    auto_corr = AutoCorrelator(5, 10, dtype=np.complex128)
+    auto_corr.write(complex_vec)
+    val = auto_corr.execute()
+
+
+def test_filter_auto_correlator_mod_l169():
+    """src/filter/auto_correlator/mod.rs:169"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    auto_corr = AutoCorrelator(5, 10, dtype=np.complex128)
+    output = auto_corr.execute_block(complex_vec)
+
+
+def test_filter_auto_correlator_mod_l197():
+    """src/filter/auto_correlator/mod.rs:197"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    auto_corr = AutoCorrelator(5, 10, dtype=np.complex128)
+    output = auto_corr.execute_block(complex_vec)
+    energy = auto_corr.get_energy()
+    _eq(_round(energy * 10000.0), 125.0)
+
+
+def test_auto_gain_control_mod_l20():
+    """src/auto_gain_control/mod.rs:20"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    agc = AGC()
+    agc.squelch_enable()
+    agc.squelch_set_threshold(-30.0)
+    agc.set_bandwidth(0.02)
+    agc_vec = agc.execute_block(complex_vec)
+    last_item = agc_vec[_len(agc_vec) - 1]
+    val = math.sqrt(last_item.real ** 2.0 + last_item.imag ** 2.0)
+    assert val > 0.98 and val < 1.02
+    assert agc.get_rssi() < -25.5 and agc.get_rssi() > -26.0
+
+
+def test_auto_gain_control_mod_l118():
+    """src/auto_gain_control/mod.rs:118"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    agc = AGC()
+    agc.squelch_enable()
+    agc.squelch_set_threshold(-30.0)
+    agc.set_bandwidth(0.01)
+    agc_vec = agc.execute_block(complex_vec)
+    assert agc.get_signal_level() < 0.05
+
+
+def test_auto_gain_control_mod_l157():
+    """src/auto_gain_control/mod.rs:157"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    agc = AGC()
+    agc.squelch_enable()
+    agc.squelch_set_threshold(-30.0)
+    agc.set_bandwidth(0.01)
+    agc_vec = agc.execute_block(complex_vec)
+    assert agc.get_gain() > 1.0
+    agc.reset()
+    assert agc.get_gain() == 1.0
+
+
+def test_auto_gain_control_mod_l194():
+    """src/auto_gain_control/mod.rs:194"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    agc = AGC()
+    agc.squelch_enable()
+    agc.squelch_set_threshold(-30.0)
+    agc.set_bandwidth(0.01)
+    agc_samp_out = agc.execute(complex_vec[0])
+    second_samp = agc.execute(complex_vec[1])
+    _eq(agc_samp_out, complex_vec[0])
+    assert _plain(second_samp) != _plain(complex_vec[1])
+
+
+def test_auto_gain_control_mod_l252():
+    """src/auto_gain_control/mod.rs:252"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    agc = AGC()
+    agc.squelch_enable()
+    agc.squelch_set_threshold(-30.0)
+    agc.set_bandwidth(0.01)
+    agc_vec = agc.execute_block(complex_vec)
+    _eq(_len(agc_vec), _len(complex_vec))
+    assert _plain(agc_vec) != _plain(complex_vec)
+    _eq(agc_vec[0], complex_vec[0])
+
+
+def test_auto_gain_control_mod_l291():
+    """src/auto_gain_control/mod.rs:291"""
+    agc = AGC()
+    _eq(agc.is_unlocked(), False)
+    agc.lock()
+    _eq(agc.is_unlocked(), True)
+    agc.unlock()
+    _eq(agc.is_unlocked(), False)
+
+
+def test_auto_gain_control_mod_l311():
+    """src/auto_gain_control/mod.rs:311"""
+    agc = AGC()
+    _eq(agc.is_unlocked(), False)
+    agc.lock()
+    _eq(agc.is_unlocked(), True)
+    agc.unlock()
+    _eq(agc.is_unlocked(), False)
+
+
+def test_auto_gain_control_mod_l330():
+    """src/auto_gain_control/mod.rs:330"""
+    agc = AGC()
+    _eq(agc.is_unlocked(), False)
+    agc.lock()
+    _eq(agc.is_unlocked(), True)
+    agc.unlock()
+    _eq(agc.is_unlocked(), False)
+
+
+def test_auto_gain_control_mod_l349():
+    """src/auto_gain_control/mod.rs:349"""
+    agc = AGC()
+    _eq(agc.get_bandwidth(), 0.1)
+
+
+def test_auto_gain_control_mod_l365():
+    """src/auto_gain_control/mod.rs:365"""
+    agc = AGC()
+    agc.set_bandwidth(0.01)
+    _eq(agc.get_bandwidth(), 0.01)
+
+
+def test_auto_gain_control_mod_l392():
+    """src/auto_gain_control/mod.rs:392"""
+    agc = AGC()
+    _eq(agc.get_signal_level(), 1.0)
+
+
+def test_auto_gain_control_mod_l408():
+    """src/auto_gain_control/mod.rs:408"""
+    agc = AGC()
+    agc.set_signal_level(10.0)
+    _eq(agc.get_signal_level(), 10.0)
+
+
+def test_auto_gain_control_mod_l434():
+    """src/auto_gain_control/mod.rs:434"""
+    agc = AGC()
+    _eq(agc.get_rssi(), -0.0)
+
+
+def test_auto_gain_control_mod_l450():
+    """src/auto_gain_control/mod.rs:450"""
+    agc = AGC()
+    agc.set_rssi(-20.0)
+    _eq(agc.get_rssi(), -20.0)
+
+
+def test_auto_gain_control_mod_l472():
+    """src/auto_gain_control/mod.rs:472"""
+    agc = AGC()
+    _eq(agc.get_gain(), 1.0)
+
+
+def test_auto_gain_control_mod_l488():
+    """src/auto_gain_control/mod.rs:488"""
+    agc = AGC()
+    agc.set_gain(2.0)
+    _eq(agc.get_gain(), 2.0)
+
+
+def test_auto_gain_control_mod_l510():
+    """src/auto_gain_control/mod.rs:510"""
+    agc = AGC()
+    _eq(agc.get_scale(), 1.0)
+
+
+def test_auto_gain_control_mod_l526():
+    """src/auto_gain_control/mod.rs:526"""
+    agc = AGC()
+    agc.set_scale(2.0)
+    _eq(agc.get_scale(), 2.0)
+
+
+def test_auto_gain_control_mod_l550():
+    """src/auto_gain_control/mod.rs:550"""
+    len = 500
+    ivec = [math.cos(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    qvec = [math.sin(float(x)) * 0.05 for x in range(int(-len / 2), int(len / 2))]
+    complex_vec = [complex(x, y) for x, y in zip(ivec, qvec)]
+    agc = AGC()
+    agc.squelch_enable()
+    agc.squelch_set_threshold(-30.0)
+    agc.set_bandwidth(0.01)
+    signal_level = agc.init(complex_vec)
+    assert signal_level > 0.04999 and signal_level <= 0.05

@@ -188,6 +188,28 @@ def test_estimate_kats():  # src/filter/firdes/mod.rs:64-69, 110-115, 161-166
     assert int((L.orc_estimate_req_filter_df(101.0, 16, 1) + 0.005) * 100.0) == 35
 
 
+def test_firdes_analysis_kats():
+    # src/filter/firdes/mod.rs doctests: firdes_doppler :376-387, filter_autocorrelation :431-441,
+    # filter_crosscorrelation :470-485, filter_isi :540-550, filter_energy :589-600 (f32 casts as there)
+    L = O.lib()
+    d = np.zeros(51)
+    L.orc_firdes_doppler(51, 0.1, 2.0, 0.0, O._dptr(d))
+    assert len(d) == 51 and np.all(np.isfinite(d))
+    h = O.firdes_notch(25, 0.2, 30.0)
+    ac = L.orc_filter_autocorrelation(O._dptr(h), len(h), 3)
+    assert ac == L.orc_filter_autocorrelation(O._dptr(h), len(h), -3)
+    assert np.float32(ac) == np.float32(0.047983058)
+    k = O.firdes_kaiser(51, 0.35, 120.0, 0.0)
+    assert np.float32(L.orc_filter_crosscorrelation(O._dptr(k), len(k), O._dptr(h), len(h), 0)) == \
+        np.float32(0.92825377)
+    rms, mx = O.C.c_double(0), O.C.c_double(0)
+    L.orc_filter_isi(O._dptr(h), len(h), 1, 25, O.C.byref(rms), O.C.byref(mx))
+    assert np.float32(rms.value) == np.float32(0.02509764) and np.float32(mx.value) == np.float32(0.061966006)
+    e = O.C.c_double(0)
+    assert L.orc_filter_energy(O._dptr(h), len(h), 0.35, 128, O.C.byref(e)) == 0
+    assert np.float32(e.value) == np.float32(0.3152318)
+
+
 def test_errors_mirror_reference():
     with pytest.raises(ValueError, match="1"):
         O.fir(O.RR64, [], 1.0)  # CoefficientsLengthZero  fir/mod.rs:80-82

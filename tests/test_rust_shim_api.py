@@ -1,9 +1,9 @@
 """The Rust shim (rust/solid-sdsp, §8f row 1) declares the reference's public API
 of the hot path exactly: for every file of src/filter/{fir,iir}/*, src/filter/mod.rs,
-src/dot_product/*, src/filter/iirdes/pll and src/fft/mod.rs, the same `pub fn` names, generic
+src/filter/firdes/*, src/filter/auto_correlator, src/dot_product/*, src/filter/iirdes/pll,
+src/fft/mod.rs, src/nco and src/auto_gain_control, the same `pub fn` names, generic
 parameters, parameter lists (names and types) and return types, the same trait
-methods and the same public structs / enums with the same variants; firdes offers a
-subset of the reference's functions with identical signatures.  The reference's
+methods and the same public structs / enums with the same variants.  The reference's
 signatures are pinned in tests/golden/reference_api.json (tools/rust_api.py); when
 /root/reference is present the fixture is regenerated and must be unchanged.
 (No cargo in this image: the shim is checked as source, not compiled.)"""
@@ -74,7 +74,8 @@ def test_shim_binds_declared_symbols_only():
 
 # C type of include/sdsp.h -> the Rust FFI type it must be declared as
 _C_SCALAR = {"int": "c_int", "size_t": "usize", "double": "f64", "float": "f32", "uint64_t": "u64",
-             "uint32_t": "u32", "int32_t": "i32", "char": "c_char", "void": "c_void"}
+             "uint32_t": "u32", "int32_t": "i32", "char": "c_char", "void": "c_void",
+             "ptrdiff_t": "isize"}
 
 
 def _c_to_rust(ctype):

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-6 GPU steps: TAG [steps...]; each step under its own limit, stop at the first failure
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+TAG=${1:-r06}; shift
+run() { local name=$1 lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${TAG}_$name.log 2>&1; local rc=$?;
+        echo "== $name rc=$rc"; grep -v amdgpu.ids gpurun_out/${TAG}_$name.log | tail -${TAILN:-30}; return $rc; }
+for step in "$@"; do
+  case $step in
+    olsab) run olsab 240 env OLS_CASES="${OLS_CASES:-24,67108888}" OLS_BURST=${OLS_BURST:-20} OLS_ROUNDS=${OLS_ROUNDS:-10} python -u tools/ols_lab.py || exit $?;;
+    iirnew) run iirnew 300 python -u -m pytest tests/test_gpu_iir.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "tiny_leading_b0 or zero_b0" || exit $?;;
+    gputests) run gputests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
+    bench) run bench 300 python bench.py --steps 20 --warmup 5 || exit $?;;
+    *) echo "unknown step $step"; exit 2;;
+  esac
+done

@@ -25,15 +25,25 @@ OUT = os.path.join(REPO, "rust", "solid-sdsp", "tests", "reference_doctests.rs")
 OUT_PY = os.path.join(REPO, "tests", "test_gpu_reference_doctests.py")
 FILES = ["filter/fir/mod.rs", "filter/fir/decim.rs", "filter/fir/interp.rs", "filter/fir/pfb.rs",
          "filter/iir/mod.rs", "filter/iir/sos.rs", "filter/iir/decim.rs", "filter/iir/interp.rs",
-         "dot_product/mod.rs", "dot_product/execute.rs"]
+         "dot_product/mod.rs", "dot_product/execute.rs",
+         # the rest of the shim's surface (firdes, AutoCorrelator, NCO, AGC)
+         "filter/firdes/mod.rs", "filter/auto_correlator/mod.rs", "nco/mod.rs", "auto_gain_control/mod.rs"]
+# files whose module-level (//!) examples are ported too
+MODULE_DOC = {"filter/auto_correlator/mod.rs", "nco/mod.rs", "auto_gain_control/mod.rs"}
 
 
-def doctests(path):
+def doctests(path, module_doc=False):
+    """```-fenced examples of the doc comments; a fence left open when its doc comment
+    ends is closed there, as rustdoc does (auto_gain_control/mod.rs:310-319)"""
     lines = open(path).read().splitlines()
     out, cur, start, inside = [], None, 0, False
     for n, l in enumerate(lines, 1):
         s = l.strip()
-        if not s.startswith("///"):
+        marker = "///" if s.startswith("///") else "//!" if module_doc and s.startswith("//!") else None
+        if marker is None:
+            if inside and s:  # blank lines stay inside a doc comment (decim.rs:272)
+                inside = False
+                out.append((start, cur))
             continue
         body = s[3:]
         if body.startswith(" "):
@@ -57,7 +67,7 @@ _DT = {"f64": "np.float64", "f32": "np.float32", "Complex<f64>": "np.complex128"
 def _statements(body):
     """split a doctest body into top-level statements (';' outside brackets / braces);
     `use` lines dropped"""
-    text = "\n".join(l for l in body if not l.strip().startswith("use "))
+    text = "\n".join(l for l in body if not l.strip().startswith(("use ", "//")))
     out, depth, cur = [], 0, ""
     for ch in text:
         if ch in "([{":
@@ -98,7 +108,17 @@ def _turbofish(s):
 
 
 def _expr(e):
-    e = re.sub(r"match (.+?) \{ Ok\((\w+)\) => \2, _ => vec!\(\) \}", r"\1", e)
+    e = re.sub(r"match (.+?) \{ Ok\((\w+)\) => \2, _ => (?:vec!\(\)|0|0\.0) \}", r"\1", e)
+    e = re.sub(r"match (.+?) \{ Ok\((\w+)\) => (.+?), _ => 0\.0 \}", r"(lambda \2: \3)(\1)", e)
+    # the AGC / AutoCorrelator doctests' test tone and its Complex zip
+    e = re.sub(r"\((-?\w+)/(\d+)\.\.(\w+)/(\d+)\)\.map\(\|(\w+)\| \(\5 as f64\)\.(cos|sin)\(\) \* ([\d.]+)\)"
+               r"\.collect\(\)", r"[math.\6(float(\5)) * \7 for \5 in range(int(\1 / \2), int(\3 / \4))]", e)
+    e = re.sub(r"(\w+)\.iter\(\)\.zip\((\w+)\.iter\(\)\)\.map\(\|\(&(\w+), &(\w+)\)\| Complex::new\(\3, \4\)\)"
+               r"\.collect\(\)", r"[complex(\3, \4) for \3, \4 in zip(\1, \2)]", e)
+    e = re.sub(r"\bAutoCorrelator::<(f64|f32)>::new\(([^()]*)\)",
+               lambda m: "AutoCorrelator(%s, dtype=%s)" % (m.group(2), _DT["Complex<%s>" % m.group(1)]), e)
+    e = re.sub(r"\b(AGC|NCO)::new\(\)", r"\1()", e)
+    e = e.replace(" && ", " and ")
     e = _turbofish(e)
     e = e.replace(".unwrap()", "").replace(".to_vec()", "")
     e = e.replace("either::Either::Right(", "(").replace("either::Either::Left(", "(")
@@ -121,6 +141,10 @@ def _expr(e):
     e = re.sub(r"\.re\b", ".real", e)
     e = re.sub(r"\.im\b", ".imag", e)
     e = re.sub(r"\b(\w+)\.len\(\)", r"_len(\1)", e)
+    e = re.sub(r"\b(\w+) as usize\b", r"int(\1)", e)
+    e = re.sub(r"\(([^()]*)\)\.round\(\)", r"_round(\1)", e)
+    e = re.sub(r"([\w.]+)\.powf\(([\d.]+)\)", r"\1 ** \2", e)
+    e = re.sub(r"\(([^()]*)\)\.sqrt\(\)", r"math.sqrt(\1)", e)
     e = re.sub(r"\bfalse\b", "False", e)
     e = re.sub(r"\btrue\b", "True", e)
     if "::" in e or "!" in e.replace("!=", "") or "&" in e:
@@ -135,9 +159,17 @@ def to_python(body):
         if m:
             out.append("%s, %s = %s" % (m.group(1), m.group(2), _expr(m.group(3))))
             continue
-        m = re.match(r"let (?:mut )?(\w+)(?:: [^=]+)? = (.+)$", st)
+        m = re.match(r"let (?:mut )?(\w+)(?:\s*: [^=]+)? = (.+)$", st)
         if m:
             out.append("%s = %s" % (m.group(1), _expr(m.group(2))))
+            continue
+        m = re.match(r"assert_eq!\((.+) as f32, (.+)\)$", st)
+        if m:  # an f32 comparison: both sides rounded to f32, as Rust compares them
+            out.append("_eq(np.float32(%s), np.float32(%s))" % (_expr(m.group(1)), _expr(m.group(2))))
+            continue
+        m = re.match(r"assert!\((\w+(?:\[\d+\])?) != (\w+(?:\[\d+\])?)\)$", st)
+        if m:  # Vec / Complex inequality, compared as values
+            out.append("assert _plain(%s) != _plain(%s)" % (_expr(m.group(1)), _expr(m.group(2))))
             continue
         m = re.match(r"assert_eq!\((.+)\)$", st)
         if m:
@@ -151,8 +183,8 @@ def to_python(body):
     return out
 
 
-PY_HEAD = '''"""The reference's doctests of the hot path (juliantos/solid-dsp src/filter/{fir,iir}/*.rs,
-src/dot_product/*.rs), translated statement by statement by tools/port_doctests.py to the
+PY_HEAD = '''"""The reference's doctests of the hot path (juliantos/solid-dsp src/filter/{fir,iir,firdes}/*.rs,
+src/filter/auto_correlator, src/dot_product/*.rs, src/nco, src/auto_gain_control), translated statement by statement by tools/port_doctests.py to the
 Python mirror of the C ABI (solid_dsp_amd) and run on the MI355X: every call goes through
 libsdsp.so, and each asserted literal is the reference's, compared exactly as Rust's
 assert_eq! compares (f64 / Complex<f64> equality).  Generated -- edit the porter, not this file."""
@@ -166,7 +198,7 @@ pytestmark = pytest.mark.gpu
 sd = pytest.importorskip("solid_dsp_amd")
 from solid_dsp_amd import (FIRFilter, DecimatingFIRFilter, InterpolatingFIRFilter, PolyPhaseFilterBank,  # noqa
                            IIRFilter, IIRFilterType, SecondOrderFilter, DecimatingIIRFilter, InterpolatingIIRFilter,
-                           DotProduct, Direction)
+                           DotProduct, Direction, AGC, NCO, AutoCorrelator)
 from solid_dsp_amd.filter import firdes, iirdes  # noqa: E402
 from solid_dsp_amd.filter.firdes import *  # noqa: E402,F401,F403
 
@@ -211,14 +243,15 @@ def _with_host_step(line):
 
 def main():
     parts = ["// Generated by tools/port_doctests.py from the reference's doc comments (juliantos/solid-dsp",
-             "// src/filter/{fir,iir}/*.rs, src/dot_product/*.rs): each doctest, body unchanged, as an",
+             "// src/filter/{fir,iir,firdes}/*.rs, src/filter/auto_correlator, src/dot_product/*.rs, src/nco,",
+             "// src/auto_gain_control): each doctest, body unchanged, as an",
              "// integration test of this crate -- the drop-in must pass the reference's own examples.",
              "// Needs libsdsp.so and a gfx950 device at run time (cargo test).", "",
              "#![allow(unused_imports, unused_variables, unused_mut)]", ""]
     total = 0
     for f in FILES:
         tag = f.replace("/", "_").replace(".rs", "")
-        for start, body in doctests(os.path.join(REF, f)):
+        for start, body in doctests(os.path.join(REF, f), f in MODULE_DOC):
             total += 1
             parts.append("/// src/%s:%d" % (f, start))
             parts.append("#[test]")
@@ -233,7 +266,7 @@ def main():
     py = [PY_HEAD]
     for f in FILES:
         tag = f.replace("/", "_").replace(".rs", "")
-        for start, body in doctests(os.path.join(REF, f)):
+        for start, body in doctests(os.path.join(REF, f), f in MODULE_DOC):
             lines = to_python(body)
             # FIR / decimator doctests also run with host_step=False, so the
             # reference's literals reach the HIP kernels (fir_step_kernel, the block kernels),

@@ -26,7 +26,11 @@ FILES = {
     "dot_product/mod.rs": ("dot_product/mod.rs", "eq"),
     "dot_product/execute.rs": ("dot_product/execute.rs", "eq"),
     "filter/iirdes/pll/mod.rs": ("filter/iirdes/pll/mod.rs", "eq"),
-    "filter/firdes/mod.rs": ("filter/firdes/mod.rs", "sub"),
+    "filter/firdes/mod.rs": ("filter/firdes/mod.rs", "eq"),
+    "filter/firdes/filter_traits.rs": ("filter/firdes/filter_traits.rs", "eq"),
+    "filter/auto_correlator/mod.rs": ("filter/auto_correlator/mod.rs", "eq"),
+    "nco/mod.rs": ("nco/mod.rs", "eq"),
+    "auto_gain_control/mod.rs": ("auto_gain_control/mod.rs", "eq"),
     "fft/mod.rs": ("fft.rs", "eq"),
 }
 
