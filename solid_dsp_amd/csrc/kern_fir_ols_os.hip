@@ -130,7 +130,8 @@ template <int ABL, bool EDGE>
 __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f2* __restrict__ hist,
                                                f2* __restrict__ new_hist, const float4* __restrict__ Hs,
                                                const float4* __restrict__ tb, f2* __restrict__ y, long long base,
-                                               long long n, int Lm1, int h2, f2* img, int t) {
+                                               long long n, int Lm1, int h2, f2* img, int t, float4 (&tq)[6],
+                                               float4 (&hq)[8], bool first = true) {
     const int hi4 = t >> 4, lo4 = t & 15;
     if constexpr ((ABL & 16) != 0) h2 = 1;  // one halo row compiled in (the launcher checks h2 == 1)
     // the segment's window x[base, base + 4096) as a raw buffer.  EDGE (the boundary segments of a
@@ -142,7 +143,8 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)(x + base), (short)0, nrec, kBufWord3);
     const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + base), (short)0, nrec, kBufWord3);
     const auto rt = __builtin_amdgcn_make_buffer_rsrc((void*)tb, (short)0, kOlsOsTabF4 * 16, kBufWord3);
-    const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0, 2048 * 16, kBufWord3);
+    const auto rh = __builtin_amdgcn_make_buffer_rsrc((void*)Hs, (short)0,
+                                                      (ABL & 268435456) ? 4 * kOlsHalfRow * 16 : 2048 * 16, kBufWord3);
     constexpr int kLdAux = (ABL & 16384) ? 0 : 2;  // nontemporal (aux 2)
     // twiddle bases: column t of W4096, row lo4 of W256 (runtime.cpp ols_build), requested
     // before the segment's rows (L2 hits that land while the rows stream in)
@@ -154,8 +156,10 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
             return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rt, 16 * lane, off, 0));
         }
     };
-    float4 tq[6];  // the raw table loads (products formed once the rows are requested)
+    // tq: the raw table loads (products formed once the rows are requested); hq: the spectrum
+    // slice.  With `first` false (a workgroup's second segment, ABL 134217728) both are reused.
     auto load_tables = [&] {
+        if (!first) return;
         if constexpr ((ABL & (32768 | 4096)) == 0) {
             tq[0] = tab(t, 16 * kOlsOsTabCD), tq[1] = tab(lo4, 16 * kOlsOsTabEF);
         } else {
@@ -212,8 +216,9 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
                 const int r = (ABL & 256) ? 15 - i : (ABL & 2097152) ? 4 * (i & 3) + (i >> 2) : i;
                 if constexpr ((ABL & 131072) != 0) v[r] = f2{0.0f, 0.0f};  // (the 16-byte-lane ablation loads its own)
                 else if constexpr (ABL & 2) v[r] = f2{1e-3f * t + r, 1e-9f * (float)base};
-                else if ((ABL & 8) && (r == 0 || r == 15))
-                    v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, 0));
+                else if ((ABL & 8) && (r == 0 || r == 15))  // 536870912: sc1 (L2 only, lab)
+                    v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r,
+                                                                                       (ABL & 536870912) ? 16 : 0));
                 else v[r] = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rx, 8 * t, 2048 * r, kLdAux));
                 if constexpr ((ABL & 16777216) != 0) __builtin_amdgcn_sched_barrier(0);  // lab: issue in this order
             }
@@ -288,11 +293,27 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
     f2* r2 = img + hi4 * kRow + lo4;  // (hi4, 16 j + lo4) at r2[17 j]
 #pragma unroll
     for (int j = 0; j < 16; ++j) v[j] = r2[17 * j];
-    float4 hq[8];  // spectrum slice of lane (k0, k1) = t for P3, k-pair major
+    // hq: the spectrum slice of lane (k0, k1) = t for P3, k-pair major.  kOlsRealTaps (real taps,
+    // H[N - k] = conj H[k]): pairs p < 4 from the half table at lane t, pairs p >= 4 as the
+    // conjugates of pair 7 - p of the mirror lane (16 - k0, 15 - k1) (k0 = 0: (0, 16 - k1); lane
+    // (0, 0): the table's tail entry), halves swapped -- a 16 KB table instead of 32 KB, read with
+    // the same eight loads (runtime.cpp ols_build)
+    constexpr bool kReal = (ABL & 268435456) != 0;
+    if constexpr (kReal) {
+        const int k0 = hi4, k1 = lo4;
+        const int ml = k0 ? 16 * (16 - k0) + (15 - k1) : (k1 ? 16 - k1 : 256);
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        if constexpr ((ABL & 2048) != 0) hq[p] = float4{1e-3f * (float)t, (float)p, 0.5f, 1e-4f * (float)t};
-        else hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+        for (int p = 0; p < 4 && first; ++p) {
+            hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 16 * kOlsHalfRow * p, 0));
+            hq[7 - p] =
+                __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * ml, 16 * kOlsHalfRow * p, 0));
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < 8 && first; ++p) {
+            if constexpr ((ABL & 2048) != 0) hq[p] = float4{1e-3f * (float)t, (float)p, 0.5f, 1e-4f * (float)t};
+            else hq[p] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rh, 16 * t, 4096 * p, 0));
+        }
     }
     f2 w2[16];  // W256^(lo4 k), used by P2 (n0 = lo4) and P3 (k1 = lo4)
 #pragma unroll
@@ -311,8 +332,13 @@ __device__ __forceinline__ void ols_os_segment(const f2* __restrict__ x, const f
         f2 u[16];
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
-            u[2 * p] = pmul(v[kout(2 * p)], f2{hq[p].x, hq[p].y});
-            u[2 * p + 1] = pmul(v[kout(2 * p + 1)], f2{hq[p].z, hq[p].w});
+            if (kReal && p >= 4) {  // {conj m.zw, conj m.xy} of the mirror's pair
+                u[2 * p] = pmulc(v[kout(2 * p)], f2{hq[p].z, hq[p].w});
+                u[2 * p + 1] = pmulc(v[kout(2 * p + 1)], f2{hq[p].x, hq[p].y});
+            } else {
+                u[2 * p] = pmul(v[kout(2 * p)], f2{hq[p].x, hq[p].y});
+                u[2 * p + 1] = pmul(v[kout(2 * p + 1)], f2{hq[p].z, hq[p].w});
+            }
         }
         idft(u);
 #pragma unroll
@@ -387,11 +413,32 @@ fir_ols_os_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, f2* __r
             const long long b = (long long)blockIdx.x - nb;
             const long long sg = b < lo ? b : hi + (b - lo);
             const long long c = blockIdx.y;
+            float4 tq[6], hq[8];
             ols_os_segment<0, true>(x + c * n, hist + c * Lm1,
                                     (new_hist != nullptr && sg == nseg - 1) ? new_hist + c * Lm1 : nullptr, Hs, tb,
-                                    y + c * n, sg * (4096 - 256 * h2) - 256 * h2, n, Lm1, h2, img, threadIdx.x);
+                                    y + c * n, sg * (4096 - 256 * h2) - 256 * h2, n, Lm1, h2, img, threadIdx.x, tq,
+                                    hq);
             return;
         }
+    }
+    const int V = 4096 - 256 * h2;
+    const long long ch = blockIdx.y;
+    float4 tq[6], hq[8];
+    if constexpr (!EDGE && (ABL & 134217728) != 0) {
+        // lab: two consecutive segments of the XCD's eighth per workgroup, the tables and the
+        // spectrum slice loaded once (half the per-segment L2 table traffic)
+        const int xc = blockIdx.x & 7;
+        const long long s0 = lo + (long long)xc * q + 2 * (long long)(blockIdx.x >> 3);
+        const long long xe0 = lo + (long long)(xc + 1) * q;
+        const long long xe = xe0 < hi ? xe0 : hi;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (s0 + k >= xe) return;  // uniform over the workgroup
+            if (k) __syncthreads();    // the first segment's P5 reads are done before P1 rewrites the image
+            ols_os_segment<ABL, false>(x + ch * n, hist + ch * Lm1, nullptr, Hs, tb, y + ch * n,
+                                       (s0 + k) * V - 256 * h2, n, Lm1, h2, img, threadIdx.x, tq, hq, k == 0);
+        }
+        return;
     }
     if constexpr (EDGE) {
         seg = (long long)blockIdx.x < lo ? (long long)blockIdx.x : hi + ((long long)blockIdx.x - lo);
@@ -403,15 +450,13 @@ fir_ols_os_kernel(const f2* __restrict__ x, const f2* __restrict__ hist, f2* __r
         const long long xe = lo + (long long)(xc + 1) * q;
         if (seg >= (xe < hi ? xe : hi)) return;  // uniform over the workgroup
     }
-    const int V = 4096 - 256 * h2;
-    const long long ch = blockIdx.y;
 #ifdef SDSP_OLS_STAMPS
     unsigned long long m0 = 0, r0 = 0;
     if constexpr ((ABL & 262144) != 0) m0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     ols_os_segment<ABL, EDGE>(x + ch * n, hist + ch * Lm1,
                               (EDGE && new_hist != nullptr && seg == nseg - 1) ? new_hist + ch * Lm1 : nullptr, Hs,
-                              tb, y + ch * n, seg * V - 256 * h2, n, Lm1, h2, img, threadIdx.x);
+                              tb, y + ch * n, seg * V - 256 * h2, n, Lm1, h2, img, threadIdx.x, tq, hq);
 #ifdef SDSP_OLS_STAMPS
     if constexpr ((ABL & 262144) != 0) {
         const unsigned long long m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -440,6 +485,7 @@ hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, const void* hist
     if (hi < lo) hi = lo;
     const long long nedge = lo + (nseg - hi);
     const long long q = (hi - lo + 7) / 8;
+    const long long qg = (ABL & 134217728) ? (q + 1) / 2 : q;  // workgroups per XCD
     if constexpr ((ABL & 33554432) != 0) {  // lab: one launch, the boundary segments past the grid
         hipLaunchKernelGGL((fir_ols_os_kernel<ABL, false>), dim3((unsigned)(8 * q + nedge), (unsigned)channels),
                            dim3(256), dyn_lds, s, (const f2*)x, (const f2*)hist, (f2*)new_hist, (const float4*)p.d_pkt,
@@ -451,8 +497,10 @@ hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, const void* hist
                        (f2*)y, (long long)n, lo, hi, 0LL, nseg, h2, Lm1);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || hi <= lo) return e;
-    hipLaunchKernelGGL((fir_ols_os_kernel<ABL, false>), dim3((unsigned)(8 * q), (unsigned)channels), dim3(256), dyn_lds,
-                       s, (const f2*)x, (const f2*)hist, (f2*)nullptr, (const float4*)p.d_pkt, (const float4*)p.d_ostab,
+    // the interior kernel's spectrum table: the half table for real taps (ABL 268435456)
+    const float4* hs = (const float4*)((ABL & 268435456) ? p.d_hhalf : p.d_pkt);
+    hipLaunchKernelGGL((fir_ols_os_kernel<ABL, false>), dim3((unsigned)(8 * qg), (unsigned)channels), dim3(256), dyn_lds,
+                       s, (const f2*)x, (const f2*)hist, (f2*)nullptr, hs, (const float4*)p.d_ostab,
                        (f2*)y, (long long)n, lo, hi, q, nseg, h2, Lm1);
     return hipGetLastError();
 }
@@ -460,10 +508,14 @@ hipError_t launch_fir_ols_os_t(const OlsPlan& p, const void* x, const void* hist
 // the interior kernel's product variants: kOlsOneHalo | kOlsHaloTemporal when the halo is one
 // row (L <= 257, every cfg2-like filter), ABL = 0 for longer filters, 524288 the 16-byte-lane form
 // (SDSP_TUNE_OLS_KERNEL = 3)
-constexpr int kOlsHaloTemporal = 8, kOlsOneHalo = 16;
+constexpr int kOlsHaloTemporal = 8, kOlsOneHalo = 16, kOlsRealTaps = 268435456;
 
 hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
                              int Lm1, size_t channels, hipStream_t s, bool wide) {
+    if (p.d_hhalf != nullptr && p.halo_rows == 1 && !wide) {
+        return launch_fir_ols_os_t<kOlsOneHalo | kOlsHaloTemporal | kOlsRealTaps>(p, x, hist, new_hist, y, n, Lm1,
+                                                                                  channels, s, 0);
+    }
     if (wide) return launch_fir_ols_os_t<524288>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0);
     if (p.halo_rows == 1)
         return launch_fir_ols_os_t<kOlsOneHalo | kOlsHaloTemporal>(p, x, hist, new_hist, y, n, Lm1, channels, s, 0);

@@ -112,7 +112,7 @@ struct sdsp_fir {
     int ols_kernel = kOlsOneShot;  // SDSP_TUNE_OLS_KERNEL
     int decim_seg = 0;  // outputs per lane group of the polyphase decimator (0 = auto)
     OlsPlan ols{};
-    DevBuf d_H, d_tw1, d_tw2, d_pkt, d_ostab;
+    DevBuf d_H, d_tw1, d_tw2, d_pkt, d_ostab, d_hhalf;
 };
 
 namespace {
@@ -243,8 +243,38 @@ int ols_build(sdsp_fir* h) {
     SDSP_TRY(h->d_ostab.ensure(os.size() * 4), "alloc one-shot tables");
     SDSP_TRY(hipMemcpyAsync(h->d_ostab.p, os.data(), os.size() * 4, hipMemcpyHostToDevice, h->stream),
              "copy one-shot tables");
+    // real taps: H[N - k] = conj(H[k]), so the one-shot kernel reads bins k2 < 8 of every lane from
+    // a half table and the others as the conjugates of its mirror lane's (kern_fir_ols_os.hip):
+    // float4 [p][i] = {H(i, 2p), H(i, 2p + 1)} for p < 4, H(i, k2) = G[k0 + 16 k1 + 256 k2] of
+    // lane i = 16 k0 + k1; entry i = 256 is the mirror of lane (0, 0), whose bins k2 >= 8 mirror
+    // k2' = 16 - k2 (k2' = 8 included): stored so that the kernel's conj-and-swap yields them
+    const bool real_taps = !coef_is_complex(h->dtype);
+    if (real_taps) {
+        std::vector<float> hh(4 * 4 * kOlsHalfRow);
+        auto set = [&](int q, int i, int half, cd v) {
+            hh[4 * (q * kOlsHalfRow + i) + 2 * half] = (float)v.re;
+            hh[4 * (q * kOlsHalfRow + i) + 2 * half + 1] = (float)v.im;
+        };
+        for (int q = 0; q < 4; ++q) {
+            for (int i = 0; i < 256; ++i) {
+                const int k0 = i >> 4, k1 = i & 15;
+                set(q, i, 0, G[k0 + 16 * k1 + 256 * (2 * q)]);
+                set(q, i, 1, G[k0 + 16 * k1 + 256 * (2 * q + 1)]);
+            }
+            // lane (0, 0), pair p = 7 - q of its bins k2 = 2p, 2p + 1: stored as
+            // {conj H(256 (2p + 1)), conj H(256 (2p))} at the mirror slot
+            const int pp = 7 - q;
+            const cd a = G[256 * (2 * pp + 1)], b = G[256 * (2 * pp)];
+            set(q, 256, 0, cd{a.re, -a.im});
+            set(q, 256, 1, cd{b.re, -b.im});
+        }
+        SDSP_TRY(h->d_hhalf.ensure(hh.size() * 4), "alloc half spectrum");
+        SDSP_TRY(hipMemcpyAsync(h->d_hhalf.p, hh.data(), hh.size() * 4, hipMemcpyHostToDevice, h->stream),
+                 "copy half spectrum");
+    }
     SDSP_TRY(hipStreamSynchronize(h->stream), "sync");
     h->ols = OlsPlan{};
+    h->ols.d_hhalf = real_taps ? h->d_hhalf.p : nullptr;
     h->ols.d_H = h->d_H.p;
     h->ols.d_tw1 = h->d_tw1.p;
     h->ols.d_tw2 = h->d_tw2.p;
@@ -550,6 +580,7 @@ void sdsp_fir_destroy(sdsp_fir* h) {
         h->d_tw2.release();
         h->d_pkt.release();
         h->d_ostab.release();
+        h->d_hhalf.release();
     }
     delete h;
 }

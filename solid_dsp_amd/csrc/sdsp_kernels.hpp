@@ -48,7 +48,11 @@ struct OlsPlan {
                               // [4096, 4224) W256 rows (runtime.cpp ols_build)
     void* d_ostab = nullptr;  // one-shot kernel tables (kOlsOsTabF4 float4, runtime.cpp ols_build)
                               // (C1 C2 | C3 D1 | D2 D3), then [16][8] float4 W256 rows
+    // real taps (conjugate-symmetric spectrum): the half-spectrum table of the one-shot kernel,
+    // float4 [4][kOlsHalfRow] (runtime.cpp ols_build), else null
+    void* d_hhalf = nullptr;
 };
+constexpr int kOlsHalfRow = 257;  // 256 lanes + the tail entry of lane (0, 0)
 constexpr int kOlsN = 4096;
 // new_hist: the next call's history buffer.  *hist_done = true when the launch also wrote it
 // (the one-shot kernel does, for n >= L - 1); otherwise the caller runs the history update.

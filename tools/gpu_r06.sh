@@ -9,6 +9,9 @@ for step in "$@"; do
   case $step in
     olsab) run olsab 240 env OLS_CASES="${OLS_CASES:-24,67108888}" OLS_BURST=${OLS_BURST:-20} OLS_ROUNDS=${OLS_ROUNDS:-10} python -u tools/ols_lab.py || exit $?;;
     iirnew) run iirnew 300 python -u -m pytest tests/test_gpu_iir.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "tiny_leading_b0 or zero_b0" || exit $?;;
+    doctests) run doctests 300 python -u -m pytest tests/test_gpu_reference_doctests.py tests/test_gpu_rx.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
+    olsiso) run olsiso 240 env OLS_CASES="${OLS_CASES:-24,67108888}" OLS_BURST=1 OLS_ROUNDS=${OLS_ROUNDS_ISO:-30} python -u tools/ols_lab.py || exit $?;;
+    firtests) run firtests 300 python -u -m pytest tests/test_gpu_fir.py tests/test_gpu_golden.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     gputests) run gputests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 || exit $?;;
     *) echo "unknown step $step"; exit 2;;
