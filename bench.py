@@ -220,9 +220,9 @@ class Cfg2FIR(StreamShard):
         self.samples_per_step = self.n
         self.bytes_per_step = 16 * self.n
         self.dtype = "c32 (f32 taps x complex-f32 samples, f32 accumulate)"
-        self.kernel = {"fft": "fir_ols_os_kernel<24, false> (one-shot XCD-ordered packed-FP32 overlap-save N=4096, "
-                              "one segment per workgroup, 4 workgroups/CU, one halo row compiled in) + "
-                              "fir_ols_os_kernel<0, true> (the 2 boundary "
+        self.kernel = {"fft": "fir_ols_os_kernel<true, false, false> (one-shot XCD-ordered packed-FP32 overlap-save N=4096, "
+                              "fused DFT16, one segment per workgroup, 4 workgroups/CU, one halo row compiled in) + "
+                              "fir_ols_os_kernel<false, false, true> (the 2 boundary "
                               "segments and the next history, a second launch)",
                        "exact": "fir_direct_kernel<EXACT>",
                        "fma": "fir_direct_kernel<FMA>"}[args.algo]

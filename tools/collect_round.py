@@ -15,7 +15,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # dispatch name to match (the interior kernel of cfg2: its boundary launch is a second
 # instance of the same template), the algo tag, and the label bench.py matches
 LABEL = {2: "fir_ols_os"}
-KERNEL = {2: ("fir_ols_os_kernel<24, false>", "fft"), 3: ("sos_wscan", "scan"),
+KERNEL = {2: ("fir_ols_os_kernel<true, false, false>", "fft"), 3: ("sos_wscan", "scan"),
           4: ("decim_poly_kernel", "fma"), 5: ("chan1024_kernel", "chan"),
           6: ("acorr_pipe_kernel", "acorr"), 7: ("nco_mix_kernel", "nco"), 8: ("fft1024_pipe", "fft"), 9: ("agc_pipe_kernel", "agc"),
           10: ("interp_tile", "interp"), 11: ("sos_serial", "iir_serial_bank"), 12: ("sos_wscan", "normal_scan")}

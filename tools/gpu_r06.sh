@@ -12,6 +12,10 @@ for step in "$@"; do
     doctests) run doctests 300 python -u -m pytest tests/test_gpu_reference_doctests.py tests/test_gpu_rx.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     olsiso) run olsiso 240 env OLS_CASES="${OLS_CASES:-24,67108888}" OLS_BURST=1 OLS_ROUNDS=${OLS_ROUNDS_ISO:-30} python -u tools/ols_lab.py || exit $?;;
     firtests) run firtests 300 python -u -m pytest tests/test_gpu_fir.py tests/test_gpu_golden.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
+    clock2) run clock2 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_BUSY_CYCLES \
+              --kernel-trace --output-format csv -d gpurun_out/${TAG}_clock_cfg2 -o run -- \
+              python bench.py --config 2 --steps 60 --warmup 5 --no-cpu --no-parity --no-dropin || exit $?;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?;;
     gputests) run gputests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 || exit $?;;
     *) echo "unknown step $step"; exit 2;;

@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-r}
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 run() { local name=$1; local lim=$2; shift 2; timeout -k 10 $lim "$@" > gpurun_out/${TAG}_$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -${TAILN:-2} gpurun_out/${TAG}_$name.log; ok $rc || exit $rc; }
-declare -A KERN=([1]=fir_direct [2]="fir_ols_os_kernel<24, false>" [3]=sos_wscan [4]=decim_poly [5]=chan1024 [6]=acorr_pipe [7]=nco_mix [8]=fft1024_pipe [9]=agc_pipe [10]=interp_tile [11]=sos_serial [12]=sos_wscan)
+declare -A KERN=([1]=fir_direct [2]="fir_ols_os_kernel<true, false, false>" [3]=sos_wscan [4]=decim_poly [5]=chan1024 [6]=acorr_pipe [7]=nco_mix [8]=fft1024_pipe [9]=agc_pipe [10]=interp_tile [11]=sos_serial [12]=sos_wscan)
 if [ -z "$SKIP_TESTS" ]; then run pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider; fi
 for c in ${CONFIGS:-2 3 4 5}; do
   run bench_cfg$c 300 python bench.py --config $c --steps 20 --warmup 5

@@ -26,6 +26,7 @@ tools/_build/lab/%.o: tools/lab/%.hip $(CSRC)/*.hpp include/sdsp.h tools/lab.mk
 $(foreach m,$(LAB_MAP),$(eval tools/_build/lab/$(word 1,$(subst :, ,$(m))).o: $(CSRC)/$(word 2,$(subst :, ,$(m))).hip))
 
 tools/_build/lab/iir_lab.o: HIPFLAGS += -fno-slp-vectorize
+tools/_build/lab/ols_lab.o: tools/lab/ols_os_lab_kernel.hip
 
 $(OUT): $(patsubst %,tools/_build/lab/%.o,$(LAB_TUS)) $(PRODUCT_OBJS)
 	$(HIPCC) --offload-arch=gfx950 -shared -fPIC -o $@.tmp $^ && mv -f $@.tmp $@
