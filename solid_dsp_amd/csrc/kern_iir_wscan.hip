@@ -223,7 +223,8 @@ template <typename I> __device__ __forceinline__ v4u to_v4(const I (&e)[16 / siz
 // 1024 compiled for one rate without exact carries, 2048 the lane shifts by one as DPP wave_shr
 // moves (real f32, D = 8), 4096 the carry as the lane scan's element -1 (no separate fold), 8192
 // compiled for 4 workgroups per CU (<= 128 VGPRs), 16384 blocks in launch order (not XCD-ordered),
-// 32768 four-wave workgroups (the form before one-wave workgroups)
+// 32768 four-wave workgroups (the form before one-wave workgroups), 65536 a segment's first tile
+// stored element by element (the form before round 6)
 template <int S, int ND, typename C, typename I, int CB, int FORM, int LAB = 0>
 __global__ void __launch_bounds__((LAB & 32768) ? kWsThreads : 64, (LAB & 8192) ? 4 : 1)
 sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -513,8 +514,15 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                                                        (pos % E) * (int)sizeof(I));
                 }
             }
-        } else if (interior && k0 >= k_lo) {
-            const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + k0), (short)0, 0x7fffffff, 0x00020000);
+        } else if (interior && (k0 >= k_lo || (LAB & (65536 | 128 | 64)) == 0)) {
+            // a segment's first tile too (it starts wc chunks early: vectors before k_lo are the
+            // warm-up's), as 16-byte stores rather than element by element (LAB 65536: the
+            // element-wise form of rounds 2-5).  The descriptor starts at max(k0, k_lo): the
+            // warm-up vectors' offsets go negative, i.e. past the descriptor's range, and the
+            // hardware drops them (chunk boundaries are 16-byte aligned) -- no branch per vector
+            const long long kb = k0 >= k_lo ? k0 : k_lo;
+            const int sh = (int)((kb - k0) * (long long)sizeof(I));
+            const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + kb), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
             for (int j = 0; j < kVecPerRow; ++j) {
                 const int v = lane + 64 * j;
@@ -524,7 +532,7 @@ sos_wscan_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict
                 // boxes, in-process A/B, profiles/r04/lab/r04b_iirab.log, r04c_iirab.log)
                 if constexpr ((lab & 128) != 0) __builtin_nontemporal_store(val, reinterpret_cast<v4u*>(y + k0) + v);
                 else if constexpr ((lab & 64) != 0) reinterpret_cast<v4u*>(y + k0)[v] = val;  // lab: plain store
-                else __builtin_amdgcn_raw_buffer_store_b128(val, ry, v * 16, 0, 16);
+                else __builtin_amdgcn_raw_buffer_store_b128(val, ry, v * 16 - sh, 0, 16);
             }
         } else {
             for (int j = 0; j < kVecPerRow; ++j) {

@@ -16,6 +16,8 @@ for step in "$@"; do
               --kernel-trace --output-format csv -d gpurun_out/${TAG}_clock_cfg2 -o run -- \
               python bench.py --config 2 --steps 60 --warmup 5 --no-cpu --no-parity --no-dropin || exit $?;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?;;
+    iirtests) run iirtests 400 python -u -m pytest tests/test_gpu_iir.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
+    libab) OLD=${OLD:-tools/_build/libsdsp_old.so} CONFIGS="${AB_CONFIGS:-3 12}" REPS=${REPS:-3} run libab 900 bash tools/lib_ab.sh ${TAG}_ab || exit $?;;
     gputests) run gputests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     bench) run bench 300 python bench.py --steps 20 --warmup 5 || exit $?;;
     *) echo "unknown step $step"; exit 2;;
