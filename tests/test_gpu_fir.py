@@ -821,3 +821,41 @@ def test_time_sharded_stream_on_device(algo, M):
         assert rel_rms(got, ref) <= 1e-6, rel_rms(got, ref)
         bound = 1e-6 * np.abs(h64).sum() * float(s) * np.abs(x64).max()
         assert np.abs(got - ref).max() <= bound, (np.abs(got - ref).max(), bound)
+
+
+def test_fir_fft_full_size_against_exact_kernel():
+    """full-size cfg2 parity in pytest, not only bench.py's four windows.  The
+    whole 2^30-sample cfg2 stream (firdes_kaiser(256, 0.1, 80), scale 0.2, device-generated) through
+    the overlap-save kernel, against the EXACT kernel on the same device buffer -- which is
+    bit-identical to the reference restatement at f32 (test_fir_exact_bit_parity and the KATs), so
+    it stands in for the oracle at a size the CPU restatement cannot reach in a test.  The §8d
+    criteria over every output: rel-RMS <= 1e-6 and max|err| <= 1e-6 * sum|h| * scale * max|x|
+    (accumulated in f64, 2^26-sample chunks)."""
+    import torch
+    n = 1 << 30
+    h = _f32_taps(256, 0.1)
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    sd.lib().sdsp_synth_f32_device(x.data_ptr(), 20250226, 0, 0, 2 * n, None)
+    y_fft = torch.empty_like(x)
+    f = FIRFilter(h, F32(0.2), sample_dtype=C64, algo=sd.ALGO_FFT)
+    assert f.execute_block_device(x, n, y_fft) == n
+    torch.cuda.synchronize()
+    y_ref = torch.empty_like(x)
+    g = FIRFilter(h, F32(0.2), sample_dtype=C64, algo=sd.ALGO_EXACT)
+    assert g.execute_block_device(x, n, y_ref) == n
+    torch.cuda.synchronize()
+    num = den = 0.0
+    worst = 0.0
+    xmax = float(x.view(torch.float32).abs().max())
+    step = 1 << 26
+    for a in range(0, n, step):
+        yf = y_fft[a:a + step].to(torch.complex128)
+        yr = y_ref[a:a + step].to(torch.complex128)
+        d = (yf - yr).abs()
+        num += float((d * d).sum())
+        den += float((yr.abs() ** 2).sum())
+        worst = max(worst, float(d.max()))
+    rel = (num / den) ** 0.5
+    assert rel <= 1e-6, rel
+    # |x| of a complex sample is at most sqrt(2) times its largest component
+    assert worst <= 1e-6 * float(np.abs(h).sum()) * 0.2 * xmax * 2 ** 0.5, worst
