@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--no-gather", action="store_true", help="skip the final RCCL gather of every rank's output")
+    p.add_argument("--dist", action="store_true",
+                   help="run the multi-GPU code path (RCCL process group, barriers, max-over-ranks, the final "
+                        "gather and its check) even at world size 1: the RCCL path on a one-GPU box")
     p.add_argument("--no-dropin", action="store_true", help="config 2: skip the drop-in cost figures")
     p.add_argument("--shard", default="channel", choices=["channel", "time"],
                    help="configs 2 and 4: independent channels per rank (default), or one long stream "
@@ -1066,17 +1069,23 @@ CPU_DEFAULT = {1: 1 << 27, 2: 1 << 26, 3: 1 << 27, 4: 1 << 28, 5: 1 << 32, 6: 1 
 CPU_CHUNK = 1 << 22
 
 
+def free_port():
+    """a free TCP port on 127.0.0.1 for a rendezvous"""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def spawn_ranks(n):
     """`--gpus N` outside torch.distributed.run: this parent never initialises the
     GPU; it starts N child ranks of this same script (one per GPU) with
     RANK / WORLD_SIZE / LOCAL_RANK and a 127.0.0.1 rendezvous, waits for all of
     them, stops the rest when one fails, and returns the worst exit status."""
-    import socket
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
@@ -1205,7 +1214,11 @@ def main():
 
     import torch
     import torch.distributed as dist
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        if "MASTER_ADDR" not in os.environ:  # --dist without a launcher: a one-rank rendezvous
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1",
+                              LOCAL_RANK="0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -1232,7 +1245,7 @@ def main():
 
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -1241,7 +1254,7 @@ def main():
         w.step(stream)
         ends[k].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     wall = time.perf_counter() - t0
     ev_ms = [s.elapsed_time(e) for s, e in zip(starts, ends)]
@@ -1250,7 +1263,7 @@ def main():
     # final gather over RCCL (timed separately, not part of `value`): every rank's
     # whole output to rank 0, checked there against the f64 restatement
     gather = None
-    if world > 1 and not args.no_gather:
+    if use_dist and not args.no_gather:
         piece = w.output() if hasattr(w, "output") else w.d_out
         torch.cuda.synchronize()
         dist.barrier()

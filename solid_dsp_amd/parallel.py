@@ -32,10 +32,11 @@ def channel_ids(per_rank: int, world_size: int, rank: int) -> list[int]:
 
 
 def max_over_ranks(value: float, device=None) -> float:
-    """The job's time is the slowest rank's (all_reduce MAX)."""
+    """The job's time is the slowest rank's (all_reduce MAX); a no-op without a process group (an
+    initialised group of one rank still runs the collective: bench.py --dist)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -62,7 +63,7 @@ def gather_full_to_root(out, root: int = 0, chunk_bytes: int = 1 << 30):
     point to point over the root's xGMI links.  Every rank passes the same numel."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return out.reshape(1, -1)
     world, rank = dist.get_world_size(), dist.get_rank()
     out = out.reshape(-1)
