@@ -101,15 +101,29 @@ constexpr int kM = 1024;
 constexpr int kRow = 18;
 constexpr int kBuf = 64 * kRow;
 
+// W1024^j from the table: the whole table (QTW false), or its first quarter rotated by
+// W1024^(256 q) = (-j)^q (QTW, the 8-transform lab form: 2 KB of LDS instead of 8)
+template <bool QTW> __device__ __forceinline__ cf tw1024(const cf* __restrict__ stw, int j) {
+    if constexpr (!QTW) {
+        return stw[j & (kM - 1)];
+    } else {
+        const cf b = stw[j & 255];
+        const int q = (j >> 8) & 3;
+        cf r = (q & 1) ? cf{b.im, -b.re} : b;
+        return (q & 2) ? cf{-r.re, -r.im} : r;
+    }
+}
+
 // P1 and P2 of one wave's 1024-point FFT: buffer holds v[p] at index p on
 // entry; on exit the P3 inputs of column c = (k2 + 16 k1) sit at buf[4 c + n0]
+template <bool QTW = false>
 __device__ __forceinline__ void fft1024_p12(cf* __restrict__ buf, const cf* __restrict__ stw, int L) {
     cf v[16];
 #pragma unroll
     for (int n2 = 0; n2 < 16; ++n2) v[n2] = buf[L + 64 * n2];
     dft16(v);
 #pragma unroll
-    for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], stw[(L * k2) & (kM - 1)]);
+    for (int k2 = 1; k2 < 16; ++k2) v[k2] = cmul(v[k2], tw1024<QTW>(stw, L * k2));
     wave_sync();
     const int n0 = L & 3, n1 = L >> 2;
 #pragma unroll
@@ -120,7 +134,7 @@ __device__ __forceinline__ void fft1024_p12(cf* __restrict__ buf, const cf* __re
     for (int i = 0; i < 16; ++i) v[i] = buf[L * kRow + i];
     dft16(v);
 #pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], stw[(16 * n0 * k1) & (kM - 1)]);
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], tw1024<QTW>(stw, 16 * n0 * k1));
     wave_sync();
     const int k2 = L >> 2;
 #pragma unroll
@@ -129,8 +143,9 @@ __device__ __forceinline__ void fft1024_p12(cf* __restrict__ buf, const cf* __re
 }
 
 // the same FFT leaving natural-order X in buf[0, 1024)
+template <bool QTW = false>
 __device__ __forceinline__ void fft1024_wave_lds(cf* __restrict__ buf, const cf* __restrict__ stw, int L) {
-    fft1024_p12(buf, stw, L);
+    fft1024_p12<QTW>(buf, stw, L);
     cf o[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -615,21 +630,27 @@ fft1024_pass_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
 // the FFT (the rest after it).
 // LA / SA: the loads' / stores' cache policy (0 default, 2 nontemporal; lab variants), LA & 8
 // the skeleton without the FFT (lab), LA / SA & 16 16-byte lanes on the strided side (LA & 16 in
-// the product), LA & 32 XCD-ordered groups (lab: 953 -> 970 us on the column pass)
+// the product), LA & 32 XCD-ordered groups (lab: 953 -> 970 us on the column pass), LA & 64 (lab)
+// neighbouring groups paired on one XCD (workgroups b and b + 8 start on groups 2P and 2P + 1,
+// so the two halves of each 2 x TPB-column run are read through one L2).  TPB = 8 (lab,
+// tools/lab/chan_lab.hip, the column pass only): 512-thread workgroups, two per CU, the W1024
+// table's first quarter in LDS (tw1024<true>: the 8 padded wave buffers and the whole table do
+// not fit twice in 160 KB)
 template <bool INV, bool TW, bool CFAST, bool OFAST, int TPB = 16, int PRE = 8, int LA = 0, int SA = 0>
 __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* __restrict__ y,
                                                   const cf* __restrict__ tw, const cf* __restrict__ twx,
                                                   long long count, long long G, long long S0, long long S1,
                                                   long long Si, long long T1, long long So) {
-    static_assert(TPB == 16, "16 transforms per workgroup");
-    constexpr int kT = 64 * TPB, kLog = 4;
+    static_assert(TPB == 16 || (TPB == 8 && CFAST && OFAST), "16 transforms per workgroup (8: the column pass)");
+    constexpr int kT = 64 * TPB, kLog = TPB == 16 ? 4 : 3;
     constexpr int kPre = PRE;
-    __shared__ cf stw[kM];
+    constexpr bool kQtw = TPB != 16;
+    __shared__ cf stw[kQtw ? 256 : kM];
     __shared__ cf sbuf[TPB * kPassBuf];
     __shared__ cf ktab[TW ? TPB * 16 : 1];
     const int t = threadIdx.x, L = t & 63, w = t >> 6;
     const long long ngroups = count / TPB;
-    stw[t] = tw[t];
+    if (!kQtw || t < 256) stw[t] = tw[t];
     auto twx_at = [&](long long m) -> cf {
         const unsigned u = (unsigned)(m & ((1 << 20) - 1));
         return cmul(twx[1024 + (u >> 10)], twx[u & 1023]);
@@ -656,8 +677,10 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
     // 16-byte than in 8-byte lanes).  SA & 16 (lab only): the same for the strided-side stores
     // (slower: 1042 us, the twiddle base per column pair costs more than the stores save)
     constexpr bool wide_in = (LA & 16) != 0 && cfast, wide_out = (SA & 16) != 0 && ofast;
-    const unsigned in_lane16 = (unsigned)(2 * (t & 7) + (long long)(t >> 3) * Si) * 8u, in_k16 = (unsigned)(128 * Si) * 8u;
-    const unsigned out_lane16 = (unsigned)(2 * (t & 7) + (long long)(t >> 3) * So) * 8u, out_k16 = (unsigned)(128 * So) * 8u;
+    // (TPB = 8: lane t holds columns 2 (t & 3), 2 (t & 3) + 1 of rows (t >> 2) + 128 m)
+    constexpr int kHm = TPB / 2 - 1, kHs = kLog - 1;
+    const unsigned in_lane16 = (unsigned)(2 * (t & kHm) + (long long)(t >> kHs) * Si) * 8u, in_k16 = (unsigned)(128 * Si) * 8u;
+    const unsigned out_lane16 = (unsigned)(2 * (t & kHm) + (long long)(t >> kHs) * So) * 8u, out_k16 = (unsigned)(128 * So) * 8u;
     typedef unsigned u2v __attribute__((ext_vector_type(2)));
     typedef unsigned u4v __attribute__((ext_vector_type(4)));
     typedef float f4v __attribute__((ext_vector_type(4)));
@@ -697,6 +720,8 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         }
     };
     long long grp = blockIdx.x;
+    if constexpr ((LA & 64) != 0)
+        if ((gridDim.x & 15) == 0) grp = ((blockIdx.x >> 4) << 4) + 2 * (blockIdx.x & 7) + ((blockIdx.x >> 3) & 1);
     if constexpr ((LA & 32) != 0)
         if ((gridDim.x & 7) == 0) grp = ((ngroups + 7) / 8) * (blockIdx.x & 7) + (blockIdx.x >> 3);
     if (grp >= last()) return;  // uniform
@@ -707,7 +732,7 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         for (int k = 0; k < 16; ++k) {
             const int e = t + kT * k;
             int c = cfast ? (e & (TPB - 1)) : (e >> 10), i = cfast ? (e >> kLog) : (e & 1023);
-            if constexpr (wide_in) c = 2 * (t & 7) + (k & 1), i = (t >> 3) + 128 * (k >> 1);
+            if constexpr (wide_in) c = 2 * (t & kHm) + (k & 1), i = (t >> kHs) + 128 * (k >> 1);
             sbuf[c * kPassBuf + i] = INV ? cf{v[k].re, -v[k].im} : v[k];
         }
         long long ib, ob, g0;
@@ -716,8 +741,8 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         if constexpr (TW) {
             if (t < TPB * 16) ktab[t] = twx_at(64 * (g0 + (t >> 4)) * (long long)(t & 15));
             if constexpr (wide_out) {
-                tbase = twx_at((g0 + 2 * (t & 7)) * (long long)(t >> 3));
-                tbase1 = twx_at((g0 + 2 * (t & 7) + 1) * (long long)(t >> 3));
+                tbase = twx_at((g0 + 2 * (t & kHm)) * (long long)(t >> kHs));
+                tbase1 = twx_at((g0 + 2 * (t & kHm) + 1) * (long long)(t >> kHs));
             } else if (ofast) {
                 tbase = twx_at((g0 + (t & (TPB - 1))) * (long long)(t >> kLog));
             }
@@ -732,7 +757,7 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
         const long long nxt = next_of(grp);
         load(nxt, 0, kPre, nxt < last());
         // LA & 8 (lab only): the pass's skeleton -- loads, staging, twiddle and stores, no FFT
-        if constexpr ((LA & 8) == 0) fft1024_wave_lds(sbuf + w * kPassBuf, stw, L);
+        if constexpr ((LA & 8) == 0) fft1024_wave_lds<kQtw>(sbuf + w * kPassBuf, stw, L);
         __syncthreads();
         load(nxt, kPre, 16, nxt < last());
         const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)(y + ob), (short)0, 0x7fffffff, 0x00020000);
@@ -742,7 +767,7 @@ __device__ __forceinline__ void fft1024_pipe_body(const cf* __restrict__ x, cf* 
                 cf r[2];
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
-                    const int c = 2 * (t & 7) + j, i = (t >> 3) + 128 * m;
+                    const int c = 2 * (t & kHm) + j, i = (t >> kHs) + 128 * m;
                     r[j] = sbuf[c * kPassBuf + i];
                     if (INV) r[j].im = -r[j].im;
                     if constexpr (TW) {
@@ -783,6 +808,7 @@ fft1024_pipe_kernel(const cf* __restrict__ x, cf* __restrict__ y, const cf* __re
                     long long Si, long long T1, long long So) {
     fft1024_pipe_body<INV, TW, CFAST, OFAST, 16, 8, LA, SA>(x, y, tw, twx, count, G, S0, S1, Si, T1, So);
 }
+
 
 }  // namespace
 

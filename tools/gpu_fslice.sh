@@ -1,0 +1,3 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+FFT_SLICES=0,8,16 FFT_ROUNDS=5 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fslice -o run -- python tools/fft_slice_ab.py > gpurun_out/fslice.log 2>&1
