@@ -51,6 +51,21 @@ __host__ __device__ constexpr int pad8(int s) { return s + (s >> 3); }
 
 template <typename T> __device__ inline cpx<T> conj_(cpx<T> a) { return {a.re, -a.im}; }
 
+// a * conj(c) with num-complex rounding (mul_(a, conj_(c)): re = a.re c.re - a.im (-c.im), im =
+// a.re (-c.im) + a.im c.re, every product rounded, no fma) in three packed instructions for c32:
+// m0 = {a.re c.re, a.re c.im}, m1 = {a.im c.im, a.im c.re}, {m0.x + m1.x, -m0.y + m1.y} -- the same
+// roundings (negation is exact, x - (-y) == x + y, the sums commute)
+template <typename T> __device__ __forceinline__ cpx<T> mul_conj_(cpx<T> a, cpx<T> c) { return mul_(a, conj_(c)); }
+template <> __device__ __forceinline__ cpx<float> mul_conj_(cpx<float> a, cpx<float> c) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v av = {a.re, a.im}, cv = {c.re, c.im};
+    f2v m0, m1, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[0,1]" : "=v"(m0) : "v"(av), "v"(cv));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[1,0]" : "=v"(m1) : "v"(av), "v"(cv));
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[1,0]" : "=v"(r) : "v"(m0), "v"(m1));
+    return {r.x, r.y};
+}
+
 
 template <typename T>
 __device__ inline cpx<T> ext_at(const cpx<T>* __restrict__ x, const cpx<T>* __restrict__ hist, long long j, int H) {
@@ -241,11 +256,12 @@ __global__ void __launch_bounds__(kTile) acorr_pipe_kernel(const cpx<T>* __restr
                 v[k] = __builtin_bit_cast(cpx<T>, __builtin_amdgcn_raw_buffer_load_b128(rx, (t + k * kTile) * kE, 0, 0));
         }
     };
+    // rows k < kOut / kTile lie inside every tile's ns = kOut + K - 1 + d staged samples: no test
     auto stage = [&] {
 #pragma unroll
         for (int k = 0; k < kLp; ++k) {
             const int i = t + k * kTile;
-            if (i < ns) xs[i] = v[k];
+            if (k < kOut / kTile || i < ns) xs[i] = v[k];
         }
     };
     load(tile, true);
@@ -258,10 +274,24 @@ __global__ void __launch_bounds__(kTile) acorr_pipe_kernel(const cpx<T>* __restr
         lds_sync();
         const long long nxt = tile + Gx;
         load(nxt, nxt < e_hi);  // in flight across this tile's products, sums and stores
+        // products: the kOut / kTile full rows with all their LDS reads issued first, then the
+        // ragged rest (cnt = kOut + K - 1)
+        {
+            constexpr int kF = kOut / kTile;
+            cpx<T> pa[kF], pc[kF];
 #pragma unroll
-        for (int k = 0; k < (kOut + kPipeK - 1 + kTile - 1) / kTile; ++k) {
-            const int s = t + k * kTile;
-            if (s < cnt) p[pad8(s)] = mul_(xs[s + d], conj_(xs[s]));
+            for (int k = 0; k < kF; ++k) {
+                const int s = t + k * kTile;
+                pa[k] = xs[s + d];
+                pc[k] = xs[s];
+            }
+#pragma unroll
+            for (int k = 0; k < kF; ++k) p[pad8(t + k * kTile)] = mul_conj_(pa[k], pc[k]);
+#pragma unroll
+            for (int k = kF; k < (kOut + kPipeK - 1 + kTile - 1) / kTile; ++k) {
+                const int s = t + k * kTile;
+                if (s < cnt) p[pad8(s)] = mul_conj_(xs[s + d], xs[s]);
+            }
         }
         lds_sync();
         cpx<T> acc[kR];

@@ -15,6 +15,12 @@ for step in "$@"; do
     clock2) run clock2 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_BUSY_CYCLES \
               --kernel-trace --output-format csv -d gpurun_out/${TAG}_clock_cfg2 -o run -- \
               python bench.py --config 2 --steps 60 --warmup 5 --no-cpu --no-parity --no-dropin || exit $?;;
+    clock) for c in ${CLOCK_CFGS:-6 9}; do
+             run clock_cfg$c 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_BUSY_CYCLES \
+               --kernel-trace --output-format csv -d gpurun_out/${TAG}_clock_cfg$c -o run -- \
+               python bench.py --config $c --steps 40 --warmup 5 --no-cpu --no-parity --no-dropin || exit $?
+           done;;
+    ffttests) run ffttests 300 python -u -m pytest tests/test_gpu_fft.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?;;
     iirtests) run iirtests 400 python -u -m pytest tests/test_gpu_iir.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     libab) OLD=${OLD:-tools/_build/libsdsp_old.so} CONFIGS="${AB_CONFIGS:-3 12}" REPS=${REPS:-3} run libab 900 bash tools/lib_ab.sh ${TAG}_ab || exit $?;;
