@@ -910,6 +910,31 @@ def dropin_costs(torch, sd, h32):
     out["f64_exact_device"] = {"Msamples_per_s": round(n / dt / 1e6, 1), "ms_per_2^26": round(dt * 1e3, 3),
                                "GBps": round(32 * n / dt / 1e9, 1), "kernel": "fir_direct_kernel<double, c64, EXACT>"}
     del xi, d_in, d_out
+    # (a') FIRFilter<f32, Complex<f32>> built with no algorithm while the process default is AUTO
+    # (SDSP_DEFAULT_ALGO=auto / sdsp_set_default_algo): an unchanged caller on the headline kernel
+    old = sd.get_default_algo()
+    sd.set_default_algo(sd.ALGO_AUTO)
+    try:
+        fa = FIRFilter(h32, np.float32(0.2), sample_dtype=np.complex64)
+    finally:
+        sd.set_default_algo(old)
+    xa = torch.empty(2 * n, dtype=torch.float32, device="cuda")
+    sd.lib().sdsp_synth_f32_device(xa.data_ptr(), SEED, 0, 0, 2 * n, st.cuda_stream)
+    d_in = torch.view_as_complex(xa.view(-1, 2))
+    d_out = torch.empty_like(d_in)
+    fa.execute_block_device(d_in, n, d_out, st)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        fa.execute_block_device(d_in, n, d_out, st)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 10
+    out["c32_default_auto_device"] = {"Msamples_per_s": round(n / dt / 1e6, 1), "ms_per_2^26": round(dt * 1e3, 3),
+                                      "algo_of_handle": int(sd.lib().sdsp_fir_get_algo(fa._h)),
+                                      "note": "FIRFilter<f32, Complex<f32>> created with no set_algo while "
+                                              "SDSP_DEFAULT_ALGO=auto: the overlap-save kernel (2^26-sample blocks, "
+                                              "host-timed, launch gaps included)"}
+    del xa, d_in, d_out, fa
     # (b) host slices through execute_block (H2D + kernel + D2H, pageable numpy buffers)
     for name, dtype, algo, m in [("host_slice_c32_fft", np.complex64, sd.ALGO_FFT, 1 << 25),
                                  ("host_slice_f64_exact", np.complex128, sd.ALGO_EXACT, 1 << 24)]:

@@ -129,6 +129,17 @@ SDSP_API int sdsp_decim_create(sdsp_fir** out, int dtype, const void* taps, size
 SDSP_API int sdsp_fir_set_channels(sdsp_fir* h, size_t channels);
 SDSP_API int sdsp_fir_set_algo(sdsp_fir* h, int algo);
 SDSP_API int sdsp_fir_get_algo(const sdsp_fir* h); /* resolved algorithm */
+/* Process-wide starting algorithm of handles created afterwards (sdsp_fir_create,
+ * sdsp_decim_create, the sdsp_iir_* / sdsp_sos_create family; PFB / interpolator handles take FMA
+ * when it is FMA, else EXACT): SDSP_ALGO_EXACT (the default: every result bit-identical to the
+ * reference), SDSP_ALGO_AUTO (blocks of >= 65536 32-bit complex samples on the overlap-save FIR,
+ * >= 65536 32-bit inputs on the FMA decimator, IIR blocks of >= 8192 samples on the scans where
+ * the cascade admits one; everything shorter on the reference order) or SDSP_ALGO_FMA.  Read from
+ * the environment variable SDSP_DEFAULT_ALGO ("auto" / "exact" / "fma") at the first handle or
+ * query unless set here first.  Not part of the reference API: it lets a deployment move an
+ * unchanged caller of that API onto the fast paths.  Existing handles keep their algorithm. */
+SDSP_API int sdsp_set_default_algo(int algo);
+SDSP_API int sdsp_get_default_algo(void);
 /* kernel-variant knobs: performance only, every accepted value computes the complete output
  * (retired keys of earlier builds are rejected with SDSP_E_INVALID_ARGUMENT). */
 typedef enum {

@@ -12,6 +12,22 @@ use std::os::raw::c_void;
 
 pub use crate::sys::{SDSP_ALGO_AUTO, SDSP_ALGO_EXACT, SDSP_ALGO_FFT, SDSP_ALGO_FMA};
 
+/// The algorithm every FIR-type and IIR handle created afterwards starts on: SDSP_ALGO_EXACT
+/// (the default, bit-identical to the reference), SDSP_ALGO_AUTO (long 32-bit blocks on the fast
+/// kernels) or SDSP_ALGO_FMA.  The environment variable SDSP_DEFAULT_ALGO ("auto" / "exact" /
+/// "fma") does the same for a whole process without a code change.
+pub fn set_default_algorithm(algo: i32) -> Result<(), Box<dyn Error>> {
+    match unsafe { sys::sdsp_set_default_algo(algo) } {
+        0 => Ok(()),
+        rc => Err(Box::new(last_error(rc))),
+    }
+}
+
+/// The starting algorithm of new handles (set_default_algorithm / SDSP_DEFAULT_ALGO)
+pub fn default_algorithm() -> i32 {
+    unsafe { sys::sdsp_get_default_algo() }
+}
+
 /// FIRFilter / DecimatingFIRFilter on the device
 pub trait FirDevice {
     /// SDSP_ALGO_EXACT (default, bit-identical), SDSP_ALGO_FMA, SDSP_ALGO_FFT (c32 FIR), SDSP_ALGO_AUTO

@@ -74,6 +74,8 @@ extern "C" {
     pub fn sdsp_fir_destroy(h: *mut sdsp_fir);
     pub fn sdsp_fir_clone(h: *const sdsp_fir, out: *mut *mut sdsp_fir) -> c_int;
     pub fn sdsp_fir_set_algo(h: *mut sdsp_fir, algo: c_int) -> c_int;
+    pub fn sdsp_set_default_algo(algo: c_int) -> c_int;
+    pub fn sdsp_get_default_algo() -> c_int;
     pub fn sdsp_fir_set_tuning(h: *mut sdsp_fir, key: c_int, value: c_int) -> c_int;
     pub fn sdsp_fir_execute(h: *mut sdsp_fir, sample: *const c_void, out: *mut c_void, n_out: *mut usize) -> c_int;
     pub fn sdsp_fir_get_state(h: *const sdsp_fir, hist: *mut c_void, phase: *mut usize) -> c_int;

@@ -26,3 +26,15 @@ __version__ = "0.1.0"
 
 def device_count() -> int:
     return int(lib().sdsp_device_count())
+
+
+def set_default_algo(algo: int) -> None:
+    """Starting algorithm of handles created from now on (ALGO_EXACT, ALGO_AUTO or ALGO_FMA;
+    sdsp_set_default_algo, include/sdsp.h).  Not part of the reference API; the environment
+    variable SDSP_DEFAULT_ALGO sets it for a whole process."""
+    from ._lib import check
+    check(lib().sdsp_set_default_algo(int(algo)))
+
+
+def get_default_algo() -> int:
+    return int(lib().sdsp_get_default_algo())

@@ -84,6 +84,8 @@ def _declare(L):
         "sdsp_fir_set_channels": (i, [vp, sz]),
         "sdsp_fir_set_algo": (i, [vp, i]),
         "sdsp_fir_get_algo": (i, [vp]),
+        "sdsp_set_default_algo": (i, [i]),
+        "sdsp_get_default_algo": (i, []),
         "sdsp_fir_set_tuning": (i, [vp, i, i]),
         "sdsp_fir_destroy": (None, [vp]),
         "sdsp_fir_clone": (i, [vp, vpp]),

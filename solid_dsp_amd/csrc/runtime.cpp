@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cctype>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -21,6 +24,27 @@ namespace sdsp {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+// Process-wide starting algorithm of new FIR-type and IIR handles: SDSP_ALGO_EXACT unless
+// sdsp_set_default_algo or the SDSP_DEFAULT_ALGO environment variable ("auto" / "exact" / "fma",
+// or 0 / 1 / 2; read once, at the first handle or query) says otherwise -- so a deployment can move
+// an unchanged reference-API caller onto the fast paths without a per-handle set_algo call.
+static std::atomic<int> g_default_algo{-1};  // -1: not yet read from the environment
+static int parse_algo_env(const char* e) {
+    if (!e) return SDSP_ALGO_EXACT;
+    std::string v(e);
+    for (auto& ch : v) ch = (char)std::tolower((unsigned char)ch);
+    if (v == "auto" || v == "0") return SDSP_ALGO_AUTO;
+    if (v == "fma" || v == "2") return SDSP_ALGO_FMA;
+    return SDSP_ALGO_EXACT;  // "exact", "1", anything else
+}
+int default_algo() {
+    int v = g_default_algo.load();
+    if (v >= 0) return v;
+    int expect = -1;
+    g_default_algo.compare_exchange_strong(expect, parse_algo_env(std::getenv("SDSP_DEFAULT_ALGO")));
+    return g_default_algo.load();
+}
 int device_status(hipError_t e, const char* what) {
     if (e == hipSuccess) return SDSP_OK;
     set_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -293,6 +317,11 @@ int fir_resolve_algo(const sdsp_fir* h, size_t n) {
     if (ols_applicable(h) && n >= (size_t)(1 << 16)) return SDSP_ALGO_FFT;
     return SDSP_ALGO_EXACT;
 }
+// AUTO on a decimating handle: the fused multiply-add kernels for long 32-bit blocks (n inputs)
+static int decim_resolve_algo(const sdsp_fir* h, size_t n) {
+    if (h->algo != SDSP_ALGO_AUTO) return h->algo;
+    return h->dtype <= SDSP_CC32 && n >= (size_t)(1 << 16) ? SDSP_ALGO_FMA : SDSP_ALGO_EXACT;
+}
 
 int fir_create_common(sdsp_fir** out, int dtype, const void* taps, size_t len, const void* scale, size_t M,
                       int device) {
@@ -320,6 +349,7 @@ int fir_create_common(sdsp_fir** out, int dtype, const void* taps, size_t len, c
     sdsp_fir* h = new sdsp_fir();
     h->dtype = dtype;
     h->device = device;
+    h->algo = default_algo();
     h->cus = info.cus;
     h->L = len;
     h->M = M;
@@ -604,6 +634,17 @@ int sdsp_fir_set_algo(sdsp_fir* h, int algo) {
 
 int sdsp_fir_get_algo(const sdsp_fir* h) { return h ? h->algo : -1; }
 
+int sdsp_set_default_algo(int algo) {
+    if (algo != SDSP_ALGO_AUTO && algo != SDSP_ALGO_EXACT && algo != SDSP_ALGO_FMA) {
+        set_error("default algorithm: SDSP_ALGO_AUTO, SDSP_ALGO_EXACT or SDSP_ALGO_FMA");
+        return SDSP_E_INVALID_ARGUMENT;
+    }
+    sdsp::g_default_algo.store(algo);
+    return SDSP_OK;
+}
+
+int sdsp_get_default_algo(void) { return sdsp::default_algo(); }
+
 int sdsp_fir_set_tuning(sdsp_fir* h, int key, int value) {
     if (!h) return SDSP_E_INVALID_ARGUMENT;
     switch (key) {
@@ -731,7 +772,7 @@ int sdsp_fir_execute_block_device(sdsp_fir* h, const void* d_in, size_t n, void*
         }
     } else {
         const size_t j0 = (h->M - 1 - h->ci) % h->M;
-        const int algo = h->algo == SDSP_ALGO_FMA ? SDSP_ALGO_FMA : SDSP_ALGO_EXACT;
+        const int algo = decim_resolve_algo(h, n) == SDSP_ALGO_FMA ? SDSP_ALGO_FMA : SDSP_ALGO_EXACT;
         FirArgs a{d_in, hist, h->d_taps_rev.p, h->scale.data(), d_out, n, nout, h->channels, (int)h->L, (int)h->M,
                   j0, algo != SDSP_ALGO_FMA};
         a.seg = h->decim_seg;
@@ -922,6 +963,7 @@ int pfb_create_common(sdsp_pfb** out, int dtype, const unsigned char* taps, size
     sdsp_pfb* h = new sdsp_pfb();
     h->dtype = dtype;
     h->device = device;
+    h->algo = default_algo() == SDSP_ALGO_FMA ? SDSP_ALGO_FMA : SDSP_ALGO_EXACT;  // (EXACT / FMA only)
     h->M = M;
     h->K = K;
     h->interp = interp;

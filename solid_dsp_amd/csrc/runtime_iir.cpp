@@ -505,6 +505,7 @@ int iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void
     sdsp_iir* h = new sdsp_iir();
     h->dtype = dtype;
     h->device = device;
+    h->algo = default_algo();
     h->type = type;
     // real f32: 128-byte chunks (B = 32; cfg3 1.75 -> 1.72 ms, its compute-only ablation 1.63 ->
     // 1.40 ms); wider samples keep 256-byte chunks so a chunk holds >= 16 samples per scan

@@ -21,6 +21,8 @@ int fir_group_delay(const std::vector<cd>& h, bool real, double f, double* out);
 int iir_group_delay(const std::vector<double>& b, const std::vector<double>& a, double f, double* out);
 
 void set_error(const std::string& msg);
+// the algorithm new FIR-type and IIR handles start on (sdsp_set_default_algo; SDSP_DEFAULT_ALGO)
+int default_algo();
 int device_status(hipError_t e, const char* what);
 
 // dtype traits (sdsp_dtype)

@@ -193,3 +193,28 @@ def test_chan_asm_checker_flags_unsafe_code():
     end = [(0x510, "s_waitcnt", " vmcnt(0)", None), (0x518, "s_endpgm", "", None)]
     assert m.check_kernel(pro + two + wait8 + first + end) == []
     assert m.check_kernel(pro + two + wait8 + second + end)
+
+
+def test_default_algo_knob_and_environment():
+    """sdsp_set_default_algo / SDSP_DEFAULT_ALGO (no device work: the knob is host state)"""
+    import sys
+    import solid_dsp_amd as sd
+    lib = sd.lib()
+    old = lib.sdsp_get_default_algo()
+    try:
+        assert lib.sdsp_set_default_algo(3) == 90  # FFT is not a default for every handle type
+        assert lib.sdsp_set_default_algo(-1) == 90 and lib.sdsp_set_default_algo(7) == 90
+        for a in (sd.ALGO_AUTO, sd.ALGO_FMA, sd.ALGO_EXACT):
+            assert lib.sdsp_set_default_algo(a) == 0 and lib.sdsp_get_default_algo() == a
+    finally:
+        lib.sdsp_set_default_algo(old)
+    code = "import solid_dsp_amd as sd; print(sd.get_default_algo())"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for env, want in (("auto", 0), ("FMA", 2), ("exact", 1), ("bogus", 1), (None, 1)):
+        e = dict(os.environ)
+        e.pop("SDSP_DEFAULT_ALGO", None)
+        if env is not None:
+            e["SDSP_DEFAULT_ALGO"] = env
+        out = subprocess.run([sys.executable, "-c", code], cwd=root, env=e, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        assert int(out.stdout.strip().splitlines()[-1]) == want, (env, out.stdout)

@@ -20,6 +20,7 @@ for step in "$@"; do
                --kernel-trace --output-format csv -d gpurun_out/${TAG}_clock_cfg$c -o run -- \
                python bench.py --config $c --steps 40 --warmup 5 --no-cpu --no-parity --no-dropin || exit $?
            done;;
+    deftests) run deftests 300 python -u -m pytest tests/test_gpu_default_algo.py tests/test_gpu_fir.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     ffttests) run ffttests 300 python -u -m pytest tests/test_gpu_fft.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?;;
     iirtests) run iirtests 400 python -u -m pytest tests/test_gpu_iir.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider || exit $?;;
