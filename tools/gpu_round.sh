@@ -17,8 +17,8 @@ for c in ${CONFIGS:-2 3 4 5}; do
   run prof_cfg$c 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof_cfg$c -o run -- python bench.py --config $c --steps 20 --warmup 5 --no-cpu --no-parity --no-dropin
   python tools/prof_summary.py gpurun_out/${TAG}_prof_cfg$c "${KERN[$c]}" --last 20 --out gpurun_out/${TAG}_kernel_timed_cfg$c.json > /dev/null 2>&1 || echo "prof_summary cfg$c failed"
   if [ -z "$SKIP_PMC" ]; then
-    run pmc_fetch_cfg$c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity --settle-ms 0
-    run pmc_write_cfg$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity --settle-ms 0
+    run pmc_fetch_cfg$c 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity --no-dropin --settle-ms 0
+    run pmc_write_cfg$c 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write_cfg$c -o run -- python bench.py --config $c --steps 3 --warmup 1 --no-cpu --no-parity --no-dropin --settle-ms 0
   fi
 done
 echo done
