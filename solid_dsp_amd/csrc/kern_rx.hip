@@ -498,77 +498,13 @@ __device__ __forceinline__ void agc_squelch(sdsp_agc_state& s, double gthr) {
     }
 }
 
-// exp(p ln E), p = -0.5 alpha in [-0.5, 0] (set_bandwidth keeps alpha in [0, 1], :374-386), for the
-// gain update's E > 1e-6.  The device libm pair costs ~130 VALU per sample (a double-double log
-// alone ~90), which made the AGC bank VALU-bound; this form takes ~45 and is as accurate as the
-// libm pair for every finite E: ln E = e ln2 + 2 atanh(s), s = f / (2 + f) with m = 1 + f in [sqrt(1/2), sqrt(2)) (12-term
-// odd series, |s| <= 0.1716), then exp by k = rint(t / ln2) and a 13-term Taylor polynomial on
-// |r| <= ln2 / 2.  Host check over 2e7 random (E, alpha): worst relative error against a long-double
-// exp(p ln E) 2.86e-14, the same as glibc's exp(p * log(E)) (both set by rounding t = p ln E at
-// |t| ~ 300), mean 7e-16.  An infinite energy (NaN never passes the caller's E > 1e-6) gives what
-// exp(p * ln(inf)) gives: 0 for p < 0, NaN for p = 0.
-__device__ __forceinline__ double agc_gain_factor(double E, double p) {
-    if (!(E < __builtin_inf())) {
-        const double t = p * E;
-        return t < 0.0 ? 0.0 : t;
-    }
-    int e;
-    double m = frexp(E, &e);  // [0.5, 1)
-    if (m < 0.70710678118654752440) {
-        m *= 2.0;
-        e -= 1;
-    }
-    const double f = m - 1.0, d = 2.0 + f;
-    double r = __builtin_amdgcn_rcp(d);
-    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-    double sv = f * r;
-    sv = __builtin_fma(__builtin_fma(-d, sv, f), r, sv);
-    const double z = sv * sv;
-    double q = 1.0 / 25;
-    q = __builtin_fma(q, z, 1.0 / 23);
-    q = __builtin_fma(q, z, 1.0 / 21);
-    q = __builtin_fma(q, z, 1.0 / 19);
-    q = __builtin_fma(q, z, 1.0 / 17);
-    q = __builtin_fma(q, z, 1.0 / 15);
-    q = __builtin_fma(q, z, 1.0 / 13);
-    q = __builtin_fma(q, z, 1.0 / 11);
-    q = __builtin_fma(q, z, 1.0 / 9);
-    q = __builtin_fma(q, z, 1.0 / 7);
-    q = __builtin_fma(q, z, 1.0 / 5);
-    q = __builtin_fma(q, z, 1.0 / 3);
-    const double s2 = 2.0 * sv;
-    const double lnm = __builtin_fma(s2 * z, q, s2);
-    constexpr double kLn2Hi = 6.93147180369123816490e-01, kLn2Lo = 1.90821492927058770002e-10;
-    const double lnE = __builtin_fma((double)e, kLn2Hi, __builtin_fma((double)e, kLn2Lo, lnm));
-    const double t = p * lnE;
-    const double k = __builtin_rint(t * 1.44269504088896338700);
-    double x = __builtin_fma(-k, kLn2Hi, t);
-    x = __builtin_fma(-k, kLn2Lo, x);
-    double y = 1.0 / 6227020800.0;  // 1/13!
-    y = __builtin_fma(y, x, 1.0 / 479001600.0);
-    y = __builtin_fma(y, x, 1.0 / 39916800.0);
-    y = __builtin_fma(y, x, 1.0 / 3628800.0);
-    y = __builtin_fma(y, x, 1.0 / 362880.0);
-    y = __builtin_fma(y, x, 1.0 / 40320.0);
-    y = __builtin_fma(y, x, 1.0 / 5040.0);
-    y = __builtin_fma(y, x, 1.0 / 720.0);
-    y = __builtin_fma(y, x, 1.0 / 120.0);
-    y = __builtin_fma(y, x, 1.0 / 24.0);
-    y = __builtin_fma(y, x, 1.0 / 6.0);
-    y = __builtin_fma(y, x, 0.5);
-    y = __builtin_fma(y, x, 1.0);
-    y = __builtin_fma(y, x, 1.0);
-    return ldexp(y, (int)k);
-}
-
 // execute  :214-246
 template <bool CPLX>
 __device__ __forceinline__ AgcSample<CPLX> agc_execute(sdsp_agc_state& s, AgcSample<CPLX> in, double gthr) {
     const AgcSample<CPLX> out = in.scaled(s.gain);
     s.energy_estimate = (1.0 - s.alpha) * s.energy_estimate + out.energy() * s.alpha;
     if (s.lock) return out;
-    if (s.energy_estimate > 0.000001) s.gain *= agc_gain_factor(s.energy_estimate, -0.5 * s.alpha);
+    if (s.energy_estimate > 0.000001) s.gain *= exp(-0.5 * s.alpha * log(s.energy_estimate));
     if (s.gain > 1000000.0) s.gain = 1000000.0;
     agc_squelch(s, gthr);
     if (s.squelch_mode == SDSP_SQUELCH_ENABLED) return in;
@@ -576,7 +512,7 @@ __device__ __forceinline__ AgcSample<CPLX> agc_execute(sdsp_agc_state& s, AgcSam
 }
 
 template <bool CPLX>
-__global__ void __launch_bounds__(64, 2) agc_kernel(const AgcSample<CPLX>* __restrict__ x, AgcSample<CPLX>* __restrict__ y,
+__global__ void __launch_bounds__(64, 4) agc_kernel(const AgcSample<CPLX>* __restrict__ x, AgcSample<CPLX>* __restrict__ y,
                                                  long long n, sdsp_agc_state* __restrict__ state, long long channels) {
     __shared__ AgcSample<CPLX> buf[64 * (kAgcS + 1)];  // row per channel, one spare slot
     const int t = threadIdx.x;
@@ -680,8 +616,7 @@ __global__ void __launch_bounds__(64) agc_pipe_kernel(const AgcSample<CPLX>* __r
     for (long long i0 = 0; i0 < nfull; i0 += S) {
         load_chunk(i0 + S);
         if (me < channels)
-#pragma unroll 1
-            for (int j = 0; j < S; ++j) {  // (not unrolled: one sample's chain is ~80 instructions)
+            for (int j = 0; j < S; ++j) {
                 AgcSample<CPLX>& v = buf[t * (S + 1) + j];
                 v = agc_execute<CPLX>(s, v, gthr);
             }
