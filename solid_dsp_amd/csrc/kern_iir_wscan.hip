@@ -1008,20 +1008,27 @@ hipError_t launch_wscan_s(const IirArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
-// Normal DF-II with D = cap - 1 states (D <= 8), 256-byte chunks
-template <typename C, typename I>
-hipError_t launch_wscan_normal(const IirArgs& a, hipStream_t st) {
+// Normal DF-II with D = cap - 1 states (D <= 8), CB-byte chunks
+template <typename C, typename I, int CB>
+hipError_t launch_wscan_normal_cb(const IirArgs& a, hipStream_t st) {
     switch (a.cap - 1) {
-        case 1: return launch_wscan_t<C, I, 0, 256, 0, 1>(a, st);
-        case 2: return launch_wscan_t<C, I, 0, 256, 0, 2>(a, st);
-        case 3: return launch_wscan_t<C, I, 0, 256, 0, 3>(a, st);
-        case 4: return launch_wscan_t<C, I, 0, 256, 0, 4>(a, st);
-        case 5: return launch_wscan_t<C, I, 0, 256, 0, 5>(a, st);
-        case 6: return launch_wscan_t<C, I, 0, 256, 0, 6>(a, st);
-        case 7: return launch_wscan_t<C, I, 0, 256, 0, 7>(a, st);
-        case 8: return launch_wscan_t<C, I, 0, 256, 0, 8>(a, st);
+        case 1: return launch_wscan_t<C, I, 0, CB, 0, 1>(a, st);
+        case 2: return launch_wscan_t<C, I, 0, CB, 0, 2>(a, st);
+        case 3: return launch_wscan_t<C, I, 0, CB, 0, 3>(a, st);
+        case 4: return launch_wscan_t<C, I, 0, CB, 0, 4>(a, st);
+        case 5: return launch_wscan_t<C, I, 0, CB, 0, 5>(a, st);
+        case 6: return launch_wscan_t<C, I, 0, CB, 0, 6>(a, st);
+        case 7: return launch_wscan_t<C, I, 0, CB, 0, 7>(a, st);
+        case 8: return launch_wscan_t<C, I, 0, CB, 0, 8>(a, st);
     }
     return hipErrorInvalidValue;
+}
+// 256-byte chunks; real f32 takes 128-byte chunks for variant 1 (its default, as for the cascades)
+template <typename C, typename I>
+hipError_t launch_wscan_normal(const IirArgs& a, hipStream_t st) {
+    if constexpr (std::is_same<I, float>::value && std::is_same<C, float>::value)
+        if (a.ws_variant == 1) return launch_wscan_normal_cb<C, I, 128>(a, st);
+    return launch_wscan_normal_cb<C, I, 256>(a, st);
 }
 
 template <typename C, typename I>

@@ -423,10 +423,14 @@ int plan_groups(sdsp_iir* h) {
         if (D < 1 || D > 8) return SDSP_OK;
         h->groups.emplace_back();
         Group& g = h->groups.back();
-        const int Bw = iir_wscan_chunk(h->dtype, 0);
-        int st = scan_tables(h, g, false, Bw, 32, 7, &g.ws[0].wc, &g.ws[0].d_P, &g.ws[0].d_Cr, &g.ws[0].d_Phi,
-                             &g.ws[0].exact);
-        if (st) return st;
+        // 256-byte chunks (variant 0), and for real f32 also 128-byte chunks (variant 1, the
+        // default there as for the SOS cascades: h->wscan = 2)
+        for (int v = 0; v < (h->dtype == SDSP_RR32 ? 2 : 1); ++v) {
+            const int Bw = iir_wscan_chunk(h->dtype, v);
+            int st = scan_tables(h, g, false, Bw, 32, 7, &g.ws[v].wc, &g.ws[v].d_P, &g.ws[v].d_Cr, &g.ws[v].d_Phi,
+                                 &g.ws[v].exact);
+            if (st) return st;
+        }
         // the kernel's coefficient layout: num[0..D] then den[0..D), zero padded
         std::vector<unsigned char> c;
         for (int i = 0; i <= D; ++i) push_coef(c, i < h->nb ? h->c64[i] : 0.0, h->dtype);
@@ -570,7 +574,11 @@ int iir_create(sdsp_iir** out, int dtype, const void* ff, size_t nff, const void
 
 // wave-scan variant index for this group (-1: none applies)
 int group_wscan(const sdsp_iir* h, const Group& g, bool rate_change) {
-    if (h->type == 0) return (h->wscan >= 1 && (g.ws[0].wc > 0 || g.ws[0].exact)) ? 0 : -1;
+    if (h->type == 0) {
+        if (h->wscan < 1) return -1;
+        const int wv = h->wscan == 2 && h->dtype == SDSP_RR32 && (g.ws[1].wc > 0 || g.ws[1].exact) ? 1 : 0;
+        return (g.ws[wv].wc > 0 || g.ws[wv].exact) ? wv : -1;
+    }
     int wv = h->wscan - 1;
     if ((rate_change || g.wc == 0) && (wv == 2 || wv == 3)) wv = 0;  // paired kernels: decaying, no rate change
     if (wv < 0) return -1;
@@ -733,18 +741,19 @@ int sdsp_iir_execute_block_device(sdsp_iir* h, const void* d_in, size_t n, void*
         bool scanned = false;
         if (!h->groups.empty() && group_scan(h, h->groups[0], nd, rc)) {  // dense-system wave scan
             Group& gr = h->groups[0];
+            const int wv = group_wscan(h, gr, rc);
             IirArgs b = a;
             b.coefs = h->d_coefs_nrm.p;
             b.algo_scan = true;
-            b.P = gr.ws[0].d_P.p;
-            b.Cr = gr.ws[0].d_Cr.p;
-            b.wc = gr.ws[0].wc;
-            b.ws_variant = 0;
+            b.P = gr.ws[wv].d_P.p;
+            b.Cr = gr.ws[wv].d_Cr.p;
+            b.wc = gr.ws[wv].wc;
+            b.ws_variant = wv;
             int tpw = 0;
             const size_t W = iir_wscan_waves(h->dtype, b, &tpw);
-            if (b.wc > 0 || exact_carry_bounded(h, gr, 0, W, tpw)) {  // else the reference-order recurrence
+            if (b.wc > 0 || exact_carry_bounded(h, gr, wv, W, tpw)) {  // else the reference-order recurrence
                 if (b.wc == 0) {
-                    b.Phi = gr.ws[0].d_Phi.p;
+                    b.Phi = gr.ws[wv].d_Phi.p;
                     const size_t bytes = h->channels * W * (size_t)(h->cap - 1) * sbytes;
                     IIR_TRY(h->d_carry[0].ensure(bytes), "iir carry scratch");
                     IIR_TRY(h->d_carry[1].ensure(bytes), "iir carry scratch");
