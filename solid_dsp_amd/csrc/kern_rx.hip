@@ -415,6 +415,9 @@ __device__ __forceinline__ cpx<T> nco_one(const T* lut, cpx<T> v, long long i, u
 // (32 KB of c32 input), issuing all its loads before staging the f32/f64 copy of
 // the sine table in LDS.
 constexpr int kNcoU = 8;
+#ifndef SDSP_NCO_WT
+#define SDSP_NCO_WT 1
+#endif
 template <typename T, bool DOWN, int V>
 __global__ void __launch_bounds__(256) nco_mix_kernel(const cpx<T>* __restrict__ x, cpx<T>* __restrict__ y, long long n,
                                                       const double* __restrict__ table, uint32_t theta0,
@@ -426,18 +429,41 @@ __global__ void __launch_bounds__(256) nco_mix_kernel(const cpx<T>* __restrict__
     Vec* yv = reinterpret_cast<Vec*>(y);
     const long long base = (long long)xcd_order(blockIdx.x, gridDim.x) * 256 * kNcoU + threadIdx.x;
     Vec r[kNcoU];
+    // 16-byte vectors (SDSP_NCO_WT): nontemporal loads and write-through (sc1) stores, the copy
+    // probe's fastest policy pair (profiles/LABLOG.md "Copy ceilings"); stores through a descriptor
+    // bounded by the call, so vectors past its end are dropped
+    constexpr bool kWt = SDSP_NCO_WT && sizeof(Vec) == 16;
+    typedef unsigned nco_u4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int u = 0; u < kNcoU; ++u)
-        if (base + 256 * u < nv) r[u] = xv[base + 256 * u];
+        if (base + 256 * u < nv) {
+            if constexpr (kWt) {
+                const nco_u4 w = __builtin_nontemporal_load(reinterpret_cast<const nco_u4*>(xv + base + 256 * u));
+                __builtin_memcpy(&r[u], &w, 16);
+            } else {
+                r[u] = xv[base + 256 * u];
+            }
+        }
     for (int i = threadIdx.x; i < 1024; i += 256) lut[i] = (T)table[i];
     __syncthreads();
+    const long long vb = base - threadIdx.x;  // the block's first vector
+    const long long vrem = nv - vb;
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(yv + (vrem > 0 ? vb : 0)), (short)0,
+        vrem <= 0 ? 0u : (unsigned)((vrem < 256LL * kNcoU ? vrem : 256LL * kNcoU) * 16), 0x00020000);
 #pragma unroll
     for (int u = 0; u < kNcoU; ++u) {
         const long long v = base + 256 * u;
         if (v < nv) {
 #pragma unroll
             for (int k = 0; k < V; ++k) r[u].s[k] = nco_one<T, DOWN>(lut, r[u].s[k], v * V + k, theta0, dtheta);
-            store_nt(yv + v, r[u]);
+            if constexpr (kWt) {
+                nco_u4 w;
+                __builtin_memcpy(&w, &r[u], 16);
+                __builtin_amdgcn_raw_buffer_store_b128(w, ry, (unsigned)(threadIdx.x + 256 * u) * 16u, 0, 16);
+            } else {
+                store_nt(yv + v, r[u]);
+            }
         }
     }
     if (blockIdx.x == 0 && threadIdx.x < n - nv * V) {  // ragged tail (c32, odd n)
