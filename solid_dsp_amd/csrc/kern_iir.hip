@@ -114,6 +114,12 @@ sos_serial_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restric
 // runs instead of one element per lane 8n bytes apart (measured 2.4x the
 // algorithmic traffic on the active_lag bank), with the next tile's loads in flight
 // while the current one runs.
+#ifndef SDSP_SERIAL_LD_AUX
+#define SDSP_SERIAL_LD_AUX 2   // tile loads: nontemporal
+#endif
+#ifndef SDSP_SERIAL_ST_AUX
+#define SDSP_SERIAL_ST_AUX 16  // tile stores: write-through (sc1)
+#endif
 template <int S, typename C, typename I>
 __global__ void __launch_bounds__(64)
 sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __restrict__ coefs,
@@ -165,7 +171,7 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
 #pragma unroll
             for (int j = 0, so = 0; j < NV; ++j, so += jstride) {
                 asm volatile("" : "+s"(so));  // formed here: not NV values hoisted into (spilled) SGPRs
-                pre[j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off0, so, 0));
+                pre[j] = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(r, off0, so, SDSP_SERIAL_LD_AUX));
             }
         };
         auto stage = [&] {
@@ -192,7 +198,8 @@ sos_serial_lds_kernel(const I* __restrict__ x, I* __restrict__ y, const C* __res
                     const int v = lane + 64 * j;
                     asm volatile("" : "+s"(so));
                     __builtin_amdgcn_raw_buffer_store_b128(
-                        *reinterpret_cast<const v4u*>(lds + (v >> kLogNV) * kRow + (v & (NV - 1)) * 16), r, off0, so, 0);
+                        *reinterpret_cast<const v4u*>(lds + (v >> kLogNV) * kRow + (v & (NV - 1)) * 16), r, off0, so,
+                        SDSP_SERIAL_ST_AUX);
                 }
                 __builtin_amdgcn_s_waitcnt(0xC07F);
                 __builtin_amdgcn_wave_barrier();
