@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(PKG, "_build", "libsdsp.so")
 RR32, RC32, CC32, RR64, RC64, CC64 = range(6)
 ALGO_AUTO, ALGO_EXACT, ALGO_FMA, ALGO_FFT = range(4)
 # sdsp_tune_key values used by the bindings (include/sdsp.h)
+TUNE_DECIM_SEG = 6
 TUNE_IIR_WAVE_SCAN, TUNE_CHAN_STREAMING, TUNE_CHAN_FRAMES_PER_BLOCK = 7, 8, 9
 TUNE_OLS_KERNEL, TUNE_CHAN_XCD_ORDER = 14, 15
 TUNE_HOST_STEP, TUNE_HOST_BLOCK_MACS = 16, 17
