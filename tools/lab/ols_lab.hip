@@ -14,7 +14,7 @@ namespace sdsp {
 
 static int g_lab_variant = 0, g_lab_lds = 0;
 
-#define SDSP_OLS_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(8) X(16) X(24) X(128) X(262168) X(2097176) X(4194328) X(132) X(256) X(260) X(512) X(768) X(772) X(1024) X(1028) X(2048) X(4096) X(6144) X(8192) X(8196) X(16384) X(16388) X(32768) X(49152) X(57344) X(131076) X(262144) X(524288) X(786432) X(2097152) X(4194304) X(6291456) X(16777216) X(18874368) X(18874880) X(33554432) X(35651584) X(67108888) X(268435480) X(65560) X(88) X(28) X(2072)
+#define SDSP_OLS_LAB_VARIANTS(X) X(1) X(2) X(3) X(4) X(8) X(16) X(24) X(128) X(262168) X(2097176) X(4194328) X(132) X(256) X(260) X(512) X(768) X(772) X(1024) X(1028) X(2048) X(4096) X(6144) X(8192) X(8196) X(16384) X(16388) X(32768) X(49152) X(57344) X(131076) X(262144) X(524288) X(786432) X(2097152) X(4194304) X(6291456) X(16777216) X(18874368) X(18874880) X(33554432) X(35651584) X(67108888) X(268435480) X(65560) X(88) X(28) X(2072) X(8216) X(152)
 
 hipError_t launch_fir_ols_os(const OlsPlan& p, const void* x, const void* hist, void* new_hist, void* y, size_t n,
                              int Lm1, size_t channels, hipStream_t s, bool wide) {
