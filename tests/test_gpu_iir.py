@@ -695,3 +695,46 @@ def test_zero_b0_section_leaves_wave_scan(dt, cdt, sdt, tol, case):
     y2 = f.execute_block(x[30000:150000])
     ref2 = o2.execute_block(_wide(x[30000:150000]))
     assert rel_rms(y2, ref2) <= tol
+
+
+def _random_cascade(rng, S, rmax):
+    """S random stable biquads: poles r e^{+-j theta} (r <= rmax), zeros rho e^{+-j phi}, gains"""
+    b, a = [], []
+    for _ in range(S):
+        r, th = rng.uniform(0.3, rmax), rng.uniform(0.05, np.pi - 0.05)
+        rho, ph = rng.uniform(0.2, 1.0), rng.uniform(0.0, np.pi)
+        g = rng.uniform(0.1, 2.0)
+        b += [g, -2.0 * g * rho * np.cos(ph), g * rho * rho]
+        a += [1.0, -2.0 * r * np.cos(th), r * r]
+    return np.array(b), np.array(a)
+
+
+@pytest.mark.parametrize("dt,cdt,sdt", [(O.RR32, np.float32, np.float32), (O.RC32, np.float32, np.complex64),
+                                        (O.RR64, np.float64, np.float64), (O.RC64, np.float64, np.complex128)])
+@pytest.mark.parametrize("seed", range(6))
+def test_wave_scan_random_cascades(dt, cdt, sdt, seed):
+    """b0-factored wave scan on random stable cascades of 1-8 sections (poles up to radius 0.97, so
+    the warm-up criterion admits them), ragged calls, against the f64 restatement: as accurate as
+    the reference-order loop at the handle's precision (rel-RMS within 10x of it, or the §8d
+    1e-5 / 1e-12), and get_state equal to the restatement's state in the reference's units"""
+    rng = np.random.default_rng(1000 + seed)
+    S = int(rng.integers(1, 9))
+    b, a = _random_cascade(rng, S, 0.97)
+    b, a = b.astype(cdt), a.astype(cdt)
+    f = IIRFilter(b, a, SO, sample_dtype=sdt, algo=sd.ALGO_FMA)
+    n = 150001
+    x = rand(rng, n, sdt)
+    cuts = [0, 3, 20000, 20001, 90000, n]
+    y = np.concatenate([f.execute_block(x[p:q]) for p, q in zip(cuts, cuts[1:])])
+    assert f.wscan_mode() in (1, 2), (S, f.wscan_mode())
+    cplx = np.dtype(sdt).kind == "c"
+    ref_dt = O.RC64 if cplx else O.RR64
+    xr = x.astype(np.complex128 if cplx else np.float64)
+    o64 = O.iir(ref_dt, b.astype(np.float64), a.astype(np.float64), O.SECOND_ORDER)
+    ref = o64.execute_block(xr)
+    tol = 1e-5 if cdt == np.float32 else 1e-12
+    tol = max(tol, 10 * rel_rms(O.iir(dt, b, a, O.SECOND_ORDER).execute_block(x), ref))
+    assert rel_rms(y, ref) <= tol, (S, rel_rms(y, ref), tol)
+    st, _ = f.get_state()  # (w1, w2) per section, the reference's units
+    st_ref = o64.sos_state()
+    assert np.abs(st.astype(st_ref.dtype) - st_ref).max() <= 100 * tol * max(1.0, np.abs(st_ref).max())
