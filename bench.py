@@ -1348,9 +1348,10 @@ def main():
                        "value": parity, "tolerance": tol, "ok": parity_ok},
             "gather": gather,
         }
-        if args.config == 2 and not args.no_dropin:
+        # the drop-in costs and the CPU baseline belong to the single-GPU line (rank 0 at N = 1)
+        if args.config == 2 and not args.no_dropin and world == 1:
             out["dropin"] = dropin_costs(torch, sd, w.h)
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:
             cb = w.cpu(args.cpu_samples or CPU_DEFAULT[args.config])
             cb["host_nproc"] = os.cpu_count()
             cb["host_affinity_cpus"] = len(os.sched_getaffinity(0))
